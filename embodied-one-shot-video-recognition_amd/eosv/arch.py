@@ -1,0 +1,110 @@
+"""ResNet backbone specs in the reference's state_dict layout.
+
+``models.model_resnet18/50`` (reference ``models.py:9-37``) wrap
+``torchvision.models.resnetXX`` minus its ``fc``: the children ``[:-1]`` become
+``self.convnet`` (``convnet.0`` conv1, ``.1`` bn1, ``.2`` relu, ``.3`` maxpool,
+``.4``-``.7`` layer1-4, ``.8`` avgpool) and a fresh ``fc`` maps the pooled
+feature to ``num_classes`` logits.  The native library builds its own layer plan
+from the same arch id (``csrc/eosv_api.cpp``); this module only supplies the
+tensor names/shapes the Python side needs.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Tuple
+
+ARCH_IDS = {"resnet18": 18, "resnet50": 50, "resnet101": 101}
+
+
+@dataclass(frozen=True)
+class ResNetSpec:
+    name: str
+    block: str            # "basic" | "bottleneck"
+    layers: Tuple[int, int, int, int]
+
+    @property
+    def expansion(self) -> int:
+        return 1 if self.block == "basic" else 4
+
+    @property
+    def feature_dim(self) -> int:
+        return 512 * self.expansion
+
+    @property
+    def arch_id(self) -> int:
+        return ARCH_IDS[self.name]
+
+
+SPECS = {
+    "resnet18": ResNetSpec("resnet18", "basic", (2, 2, 2, 2)),
+    "resnet50": ResNetSpec("resnet50", "bottleneck", (3, 4, 6, 3)),
+    "resnet101": ResNetSpec("resnet101", "bottleneck", (3, 4, 23, 3)),
+}
+
+
+def _bn(prefix: str, c: int, out: Dict[str, tuple]):
+    out[prefix + ".weight"] = (c,)
+    out[prefix + ".bias"] = (c,)
+    out[prefix + ".running_mean"] = (c,)
+    out[prefix + ".running_var"] = (c,)
+    out[prefix + ".num_batches_tracked"] = ()
+
+
+def state_dict_shapes(spec: ResNetSpec, num_classes: int = 64) -> Dict[str, tuple]:
+    """Ordered name -> shape of ``model_resnetXX(num_classes).state_dict()``."""
+    out: Dict[str, tuple] = {}
+    out["convnet.0.weight"] = (64, 3, 7, 7)
+    _bn("convnet.1", 64, out)
+    inplanes = 64
+    for li, (planes, n) in enumerate(zip((64, 128, 256, 512), spec.layers)):
+        for bi in range(n):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            p = f"convnet.{4 + li}.{bi}"
+            if spec.block == "basic":
+                out[p + ".conv1.weight"] = (planes, inplanes, 3, 3)
+                _bn(p + ".bn1", planes, out)
+                out[p + ".conv2.weight"] = (planes, planes, 3, 3)
+                _bn(p + ".bn2", planes, out)
+            else:
+                out[p + ".conv1.weight"] = (planes, inplanes, 1, 1)
+                _bn(p + ".bn1", planes, out)
+                out[p + ".conv2.weight"] = (planes, planes, 3, 3)
+                _bn(p + ".bn2", planes, out)
+                out[p + ".conv3.weight"] = (planes * 4, planes, 1, 1)
+                _bn(p + ".bn3", planes * 4, out)
+            cout = planes * spec.expansion
+            if bi == 0 and (stride != 1 or inplanes != cout):
+                out[p + ".downsample.0.weight"] = (cout, inplanes, 1, 1)
+                _bn(p + ".downsample.1", cout, out)
+            inplanes = cout
+    out["fc.weight"] = (num_classes, spec.feature_dim)
+    out["fc.bias"] = (num_classes,)
+    return out
+
+
+def conv_macs_per_frame(spec: ResNetSpec, H: int = 224, W: int = 224) -> int:
+    """Multiply-accumulates of every conv of the backbone for one frame."""
+    def out_hw(h, k, s, p):
+        return (h + 2 * p - k) // s + 1
+
+    macs = 0
+    h, w = out_hw(H, 7, 2, 3), out_hw(W, 7, 2, 3)
+    macs += h * w * 64 * 3 * 49
+    h, w = out_hw(h, 3, 2, 1), out_hw(w, 3, 2, 1)
+    inplanes = 64
+    for li, (planes, n) in enumerate(zip((64, 128, 256, 512), spec.layers)):
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            cout = planes * spec.expansion
+            ho, wo = out_hw(h, 3, s, 1), out_hw(w, 3, s, 1)
+            if spec.block == "basic":
+                macs += ho * wo * planes * inplanes * 9 + ho * wo * planes * planes * 9
+            else:
+                macs += h * w * planes * inplanes          # 1x1 at input res
+                macs += ho * wo * planes * planes * 9       # 3x3 (stride here)
+                macs += ho * wo * cout * planes              # 1x1 expand
+            if bi == 0 and (s != 1 or inplanes != cout):
+                macs += ho * wo * cout * inplanes
+            h, w = ho, wo
+            inplanes = cout
+    return macs

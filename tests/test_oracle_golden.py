@@ -1,0 +1,63 @@
+"""Pin the CPU oracle against vectors captured from the reference itself.
+
+Fixtures come from tests/golden/capture_golden.py, which ran the reference's own
+EpisodeDataloader / TestNetwork / Classifier code in the build container.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from _common import load_fixture, load_video
+from eosv import arch, synth
+from oracle import harness_ref, resnet_ref
+
+REF_LIST = None
+
+
+def _test_list():
+    import os
+    p = os.path.join(os.path.dirname(__file__), "golden", "test.list")
+    return open(p).readlines()
+
+
+def test_episode_plans_match_reference_rng_order():
+    meta, _ = load_fixture("plans_test_seed0")
+    d = harness_ref.class_index(_test_list())
+    rnd = random.Random(meta["seed"])
+    for ep in meta["episodes"]:
+        plan = harness_ref.sample_episode_plan(d, meta["n_way"], meta["k_shot"], rnd)
+        assert plan["support"] == ep["support"]
+        assert plan["query"] == ep["query"]
+        assert plan["support_y"] == ep["support_y"]
+        assert plan["query_y"] == ep["query_y"]
+
+
+def test_frame_counts_match_reference_loader():
+    meta, _ = load_fixture("c1_r18_protonet_seed1")
+    for ep in meta["episodes"]:
+        for vi, n in zip(ep["support"], ep["support_frames"]):
+            assert load_video(vi, True)[1] == n
+        assert load_video(ep["query"], False)[1] == ep["query_frames"]
+
+
+def test_acc_file_format():
+    meta, arr = load_fixture("c1_r18_protonet_seed1")
+    accs = [float(np.mean(np.array([e["query_y"]]) == p)) for e, p in zip(meta["episodes"], arr["pred"])]
+    assert "\n".join(harness_ref.acc_lines(accs)) + "\n" == meta["acc_file"]
+
+
+@pytest.mark.parametrize("tag", ["c1_r18_protonet_seed1", "c1_r18_cosine_seed2", "c1_r50_protonet_seed3"])
+def test_oracle_harness_matches_reference(tag):
+    torch.set_num_threads(8)
+    meta, arr = load_fixture(tag)
+    sd = synth.synth_state_dict(arch.SPECS[meta["arch"]], 64, 0)
+    model = resnet_ref.build_model(meta["arch"], sd)
+    res = harness_ref.run_baseline(model, meta["episodes"], load_video, L2=True, kind=meta["classifier"])
+    for i, r in enumerate(res):
+        np.testing.assert_allclose(r["support_feature"], arr["support_feature"][i], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(r["query_feature"], arr["query_feature"][i], rtol=1e-5, atol=1e-7)
+        assert np.array_equal(r["pred"], arr["pred"][i])
+    accs = [r["acc"] for r in res]
+    assert "\n".join(harness_ref.acc_lines(accs)) + "\n" == meta["acc_file"]
