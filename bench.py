@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Headline benchmark: clips/s of the clip-embedding + one-shot matching path.
+
+Workload (BASELINE.json configs[1], the metric's config): 5-way 1-shot episodes
+sampled from the reference's test.list in the reference's RNG order, 8 segments x
+seg_len 2 = 16 frames per clip at 224x224, ResNet-18 backbone, f32 arithmetic,
+synthetic frames generated in HBM before the timed region.
+
+One "step" = one batch of --episodes-per-step episodes per rank: every frame of
+every clip through the backbone (one batched call), L2 + temporal mean per clip,
+protonet matching of every episode.  Episodes are sharded e % world == rank; the
+per-rank predictions are all-gathered once (RCCL) after the timed region.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md section "Measurement".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "embodied-one-shot-video-recognition_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+MFMA_PEAK_TF = {"f32": 157.3, "bf16": 2516.6}  # MI355X dense peaks (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--episodes-per-step", type=int, default=100)
+    ap.add_argument("--arch", default="resnet18")
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--res", type=int, default=224)
+    ap.add_argument("--n-way", type=int, default=5)
+    ap.add_argument("--k-shot", type=int, default=1)
+    ap.add_argument("--segments", type=int, default=8)
+    ap.add_argument("--seg-len", type=int, default=2)
+    ap.add_argument("--max-frames", type=int, default=1024)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-baseline-sec", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, episodes, T):
+    """Oracle (fp32 torch-CPU restatement of the reference path) on a bounded sample."""
+    sys.path.insert(0, REPO)
+    from eosv import arch as arch_mod, synth  # noqa
+    from oracle import harness_ref, resnet_ref  # noqa  (checker / CPU baseline only)
+
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    model = resnet_ref.build_model(args.arch, synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
+
+    def load(vi, support):
+        ids, n_all = synth.clip_frame_ids(vi, T)
+        v = torch.from_numpy(synth.synth_video(vi.split("/")[0], vi, ids, args.res, args.res))
+        return v, v.shape[0]
+
+    t_load = 0.0
+    clips = frames = done = 0
+    t0 = time.perf_counter()
+    for ep in episodes:
+        tl = time.perf_counter()
+        vids = [load(v, True) for v in ep["support"]] + [load(ep["query"], False)]
+        t_load += time.perf_counter() - tl
+        sx = [v for v, _ in vids[:-1]]
+        sf = [n for _, n in vids[:-1]]
+        harness_ref.epoch_features(model, sx, True, sf)
+        harness_ref.epoch_features(model, [vids[-1][0]], True)
+        clips += len(vids)
+        frames += sum(n for _, n in vids)
+        done += 1
+        if time.perf_counter() - t0 - t_load > args.cpu_baseline_sec:
+            break
+    el = time.perf_counter() - t0 - t_load
+    return {"value": round(clips / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"{done} episodes ({clips} clips, {frames} frames) of the same workload through "
+                      f"oracle/ (torch-CPU fp32 restatement of network_test.py:49-68 + classifier.py), "
+                      f"synthetic-frame generation excluded; {el:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from eosv import arch as arch_mod, engine, episodes as ep_mod, synth  # noqa
+
+    T = args.segments * args.seg_len
+    E = args.episodes_per_step
+    n_steps = args.warmup + args.steps
+    plans = ep_mod.sample_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed)
+    mine = ep_mod.shard(plans, rank, world)
+    bb = engine.Backbone(args.arch, args.dtype, args.res, args.res, max_frames=args.max_frames,
+                         device=local)
+    bb.load_state_dict(synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
+    batches = []
+    for s in range(n_steps):
+        b = engine.build_episode_batch(mine[s * E:(s + 1) * E], T)
+        batches.append(engine.DeviceEpisodes(b, args.res, args.res, device=local))
+    feat = torch.empty(max(d.batch.n_frames for d in batches), bb.D, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    preds = []
+    for s in range(args.warmup):
+        d = batches[s]
+        p, _, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    bb.profile(True)
+    t0 = time.perf_counter()
+    for s in range(args.warmup, n_steps):
+        d = batches[s]
+        p, _, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
+        preds.append(p)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms, fl, nl = bb.profile_read()
+    bb.profile(False)
+
+    clips = sum(d.batch.n_clips for d in batches[args.warmup:])
+    frames = sum(d.batch.n_frames for d in batches[args.warmup:])
+    # results: (pred, correct) per episode, all-gathered over xGMI
+    pred = torch.cat(preds)
+    qy = torch.from_numpy(np.concatenate([d.batch.query_y for d in batches[args.warmup:]])).to(pred.device)
+    res = torch.stack([pred.to(torch.int32), (pred == qy).to(torch.int32)], 1)
+    if dist:
+        el_t = torch.tensor([elapsed], device=pred.device, dtype=torch.float64)
+        tdist.all_reduce(el_t, op=tdist.ReduceOp.MAX)
+        elapsed = float(el_t.item())
+        tot = torch.tensor([clips, frames], device=pred.device, dtype=torch.int64)
+        tdist.all_reduce(tot)
+        clips, frames = int(tot[0]), int(tot[1])
+        gathered = [torch.empty_like(res) for _ in range(world)]
+        tdist.all_gather(gathered, res)
+        res = torch.cat(gathered)
+    acc = float(res[:, 1].float().mean().item())
+
+    if rank == 0:
+        conv_ms, conv_fl = float(ms.sum()), float(fl.sum())
+        launches = int(nl.sum())
+        achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        peak = MFMA_PEAK_TF[args.dtype]
+        gflop_frame = 2 * arch_mod.conv_macs_per_frame(arch_mod.SPECS[args.arch], args.res, args.res) / 1e9
+        out = {
+            "metric": "clips/sec/GPU (224², 8-seg) + 5-way-1-shot episode acc vs reference",
+            "value": round(clips / elapsed, 2),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic frames (deterministic, generated in HBM) + random-init weights of the "
+                    "reference architecture; episodes from the reference's test.list in its RNG order",
+            "config": {"workload": f"test_network_baseline {args.n_way}-way {args.k_shot}-shot, "
+                                   f"{args.segments} seg x {args.seg_len} frames, {args.arch}, "
+                                   f"{args.res}x{args.res}, {args.dtype} (BASELINE configs[1])",
+                       "episodes_per_step_per_gpu": E, "episodes_timed": E * args.steps * world,
+                       "frames_per_clip": T, "parallelism": f"episode-sharded dp{world}"},
+            "frames_per_s": round(frames / elapsed, 1),
+            "episode_acc": round(acc, 4),
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "kernel": f"conv_{args.dtype}_kernel (all {launches} conv launches of the timed "
+                                   f"region, HIP events on the launch stream)",
+                         "flop_per_frame": round(gflop_frame * 1e9),
+                         "end_to_end_tflops": round(frames * gflop_frame / elapsed / 1e3, 2)},
+            "cpu_baseline": None,
+        }
+        if args.layers:
+            for i in range(len(ms)):
+                if nl[i]:
+                    print(f"layer {i:3d}: {ms[i] / nl[i]:8.3f} ms/launch  {fl[i] / ms[i] / 1e9:7.2f} TF/s",
+                          file=sys.stderr)
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args, mine[:50], T)
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,57 @@
+// Internal helpers shared by the eosv HIP translation units (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "eosv.h"
+
+#include <cstdint>
+#include <string>
+
+namespace eosv {
+
+void set_error(const std::string& msg);
+
+#define EOSV_HIP_CHECK(expr)                                                               \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess) {                                                                \
+      ::eosv::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));               \
+      return EOSV_ERR_HIP;                                                                 \
+    }                                                                                      \
+  } while (0)
+
+#define EOSV_LAUNCH_CHECK()                                                                \
+  do {                                                                                     \
+    hipError_t _e = hipGetLastError();                                                     \
+    if (_e != hipSuccess) {                                                                \
+      ::eosv::set_error(std::string("kernel launch: ") + hipGetErrorString(_e));          \
+      return EOSV_ERR_HIP;                                                                 \
+    }                                                                                      \
+  } while (0)
+
+// ------------------------------------------------------------------ conv
+struct ConvArgs {
+  const void* x;      // NHWC input [N,H,W,Cin]  (stem: Cin = 4, channel 3 zero)
+  const void* w;      // [Cout][K]: K ordered (kh, kw_padded, cin)
+  const float* bias;  // [Cout] folded BN shift
+  const void* res;    // NHWC residual [N,Ho,Wo,Cout] or nullptr
+  void* y;            // NHWC output [N,Ho,Wo,Cout]
+  int N, H, W, Cin;
+  int Ho, Wo, Cout;
+  int KH, KW, KWp, stride, pad;
+  int K;              // padded reduction length, multiple of the kernel's BK
+  int relu;
+};
+
+int launch_conv_f32(const ConvArgs& a, hipStream_t s);
+int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ layout / pooling
+int launch_pack_nchw_nhwc4(const float* x, int B, int H, int W, void* y, int bf16,
+                           hipStream_t s);
+int launch_maxpool3x3s2(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo,
+                        int bf16, hipStream_t s);
+int launch_avgpool(const void* x, int B, int HW, int C, float* y, int bf16, hipStream_t s);
+
+}  // namespace eosv

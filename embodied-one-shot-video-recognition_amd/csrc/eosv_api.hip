@@ -1,0 +1,467 @@
+// eosv C ABI: handle lifecycle, weight folding and the backbone layer plan.
+//
+// The native runtime owns what torchvision/cuDNN owned in the reference
+// (models.py:9-37): the ResNet layer plan (built from the arch id, torchvision v1.5
+// structure), BN folded into conv weights at load time, NHWC workspaces sized for
+// max_frames, and the per-chunk launch sequence
+//   pack NCHW->NHWC4 -> stem conv (+BN+ReLU) -> maxpool -> blocks (conv+BN[+ReLU],
+//   residual add + ReLU fused into the last conv's epilogue) -> avgpool.
+#include <hip/hip_bf16.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace eosv {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+struct Conv {
+  int cin = 0, cout = 0, kh = 1, kw = 1, kwp = 1, cinp = 0, stride = 1, pad = 0, K = 0;
+  bool stem = false;
+  int id = 0;                 // layer id for profiling (plan order)
+  std::string wname, bnname;  // state_dict prefixes
+  void* w = nullptr;          // [cout][K] (f32 or bf16)
+  float* b = nullptr;         // [cout]
+};
+
+struct Block {
+  bool bottleneck = false, has_ds = false;
+  Conv c1, c2, c3, ds;
+};
+
+}  // namespace eosv
+
+struct eosv_handle {
+  eosv_desc d{};
+  int D = 0;
+  int hs = 0, ws = 0, hp = 0, wp = 0;  // stem / maxpool output sizes
+  eosv::Conv stem, fc;
+  std::vector<eosv::Block> blocks;
+  bool loaded = false;
+  size_t act_elems = 0;  // per-frame max activation elements
+  void* pack = nullptr;
+  void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<void*> allocs;
+  int64_t bytes = 0;
+  int n_layers = 0;
+  // profiling (eosv_profile_enable/read)
+  struct Rec {
+    int id;
+    hipEvent_t a, b;
+    double flops;
+  };
+  bool prof = false;
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
+};
+
+namespace eosv {
+
+static int conv_out(int h, int k, int s, int p) { return (h + 2 * p - k) / s + 1; }
+
+static Conv make_conv(int cin, int cout, int k, int stride, int pad, const std::string& wname,
+                      const std::string& bnname) {
+  Conv c;
+  c.cin = cin;
+  c.cout = cout;
+  c.kh = c.kw = c.kwp = k;
+  c.cinp = cin;
+  c.stride = stride;
+  c.pad = pad;
+  c.K = k * k * cin;
+  c.wname = wname;
+  c.bnname = bnname;
+  return c;
+}
+
+static int build_plan(eosv_handle* h) {
+  const int arch = h->d.arch;
+  int layers[4];
+  bool bottleneck;
+  if (arch == EOSV_ARCH_R18) {
+    bottleneck = false;
+    int l[4] = {2, 2, 2, 2};
+    memcpy(layers, l, sizeof l);
+  } else if (arch == EOSV_ARCH_R50) {
+    bottleneck = true;
+    int l[4] = {3, 4, 6, 3};
+    memcpy(layers, l, sizeof l);
+  } else if (arch == EOSV_ARCH_R101) {
+    bottleneck = true;
+    int l[4] = {3, 4, 23, 3};
+    memcpy(layers, l, sizeof l);
+  } else {
+    set_error("eosv_create: unsupported arch (18, 50, 101)");
+    return EOSV_ERR_UNSUPPORTED;
+  }
+  const int exp = bottleneck ? 4 : 1;
+  h->D = 512 * exp;
+  // stem: 7x7/2 p3, Cin 3 padded to 4, kw padded to 8 -> K = 7*8*4 = 224
+  Conv st = make_conv(3, 64, 7, 2, 3, "convnet.0.weight", "convnet.1");
+  st.stem = true;
+  st.kwp = 8;
+  st.cinp = 4;
+  st.K = 7 * 8 * 4;
+  h->stem = st;
+  h->hs = conv_out(h->d.height, 7, 2, 3);
+  h->ws = conv_out(h->d.width, 7, 2, 3);
+  h->hp = conv_out(h->hs, 3, 2, 1);
+  h->wp = conv_out(h->ws, 3, 2, 1);
+  size_t act = (size_t)h->hs * h->ws * 64;
+  int hh = h->hp, ww = h->wp, inpl = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int planes = 64 << li;
+    for (int bi = 0; bi < layers[li]; ++bi) {
+      const int s = (li > 0 && bi == 0) ? 2 : 1;
+      const std::string p = "convnet." + std::to_string(4 + li) + "." + std::to_string(bi);
+      Block b;
+      b.bottleneck = bottleneck;
+      const int cout = planes * exp;
+      const int ho = conv_out(hh, 3, s, 1), wo = conv_out(ww, 3, s, 1);
+      if (!bottleneck) {
+        b.c1 = make_conv(inpl, planes, 3, s, 1, p + ".conv1.weight", p + ".bn1");
+        b.c2 = make_conv(planes, planes, 3, 1, 1, p + ".conv2.weight", p + ".bn2");
+        act = std::max(act, (size_t)ho * wo * planes);
+      } else {
+        b.c1 = make_conv(inpl, planes, 1, 1, 0, p + ".conv1.weight", p + ".bn1");
+        b.c2 = make_conv(planes, planes, 3, s, 1, p + ".conv2.weight", p + ".bn2");
+        b.c3 = make_conv(planes, cout, 1, 1, 0, p + ".conv3.weight", p + ".bn3");
+        act = std::max(act, (size_t)hh * ww * planes);
+        act = std::max(act, (size_t)ho * wo * cout);
+      }
+      if (bi == 0 && (s != 1 || inpl != cout)) {
+        b.has_ds = true;
+        b.ds = make_conv(inpl, cout, 1, s, 0, p + ".downsample.0.weight", p + ".downsample.1");
+      }
+      h->blocks.push_back(b);
+      hh = ho;
+      ww = wo;
+      inpl = cout;
+    }
+  }
+  h->act_elems = act;
+  Conv fc = make_conv(h->D, h->d.num_classes, 1, 1, 0, "fc.weight", "");
+  h->fc = fc;
+  int id = 0;
+  h->stem.id = id++;
+  for (Block& b : h->blocks) {
+    b.c1.id = id++;
+    b.c2.id = id++;
+    if (b.bottleneck) b.c3.id = id++;
+    if (b.has_ds) b.ds.id = id++;
+  }
+  h->fc.id = id++;
+  h->n_layers = id;
+  return EOSV_OK;
+}
+
+static int dmalloc(eosv_handle* h, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    set_error("hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? EOSV_ERR_OOM : EOSV_ERR_HIP;
+  }
+  h->allocs.push_back(*p);
+  h->bytes += (int64_t)bytes;
+  return EOSV_OK;
+}
+
+static unsigned short f2bf_host(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+struct Tensors {
+  std::unordered_map<std::string, std::pair<const float*, int64_t>> m;
+  const float* get(const std::string& n, int64_t numel) const {
+    auto it = m.find(n);
+    if (it == m.end()) {
+      set_error("eosv_load_weights: missing tensor '" + n + "'");
+      return nullptr;
+    }
+    if (it->second.second != numel) {
+      set_error("eosv_load_weights: tensor '" + n + "' has " + std::to_string(it->second.second) +
+                " elements, expected " + std::to_string(numel));
+      return nullptr;
+    }
+    return it->second.first;
+  }
+};
+
+// fold BN (eval) into the conv and upload [cout][K] weights + [cout] bias
+static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, bool has_bn) {
+  const float* w = t.get(c.wname, (int64_t)c.cout * c.cin * c.kh * c.kw);
+  if (!w) return EOSV_ERR_ARG;
+  std::vector<float> alpha(c.cout, 1.f), beta(c.cout, 0.f);
+  if (has_bn) {
+    const float* g = t.get(c.bnname + ".weight", c.cout);
+    const float* bb = t.get(c.bnname + ".bias", c.cout);
+    const float* mu = t.get(c.bnname + ".running_mean", c.cout);
+    const float* var = t.get(c.bnname + ".running_var", c.cout);
+    if (!g || !bb || !mu || !var) return EOSV_ERR_ARG;
+    for (int o = 0; o < c.cout; ++o) {
+      // same arithmetic as torch's CPU BN inference: alpha = gamma / sqrt(var + eps)
+      alpha[o] = (1.f / std::sqrt(var[o] + 1e-5f)) * g[o];
+      beta[o] = bb[o] - mu[o] * alpha[o];
+    }
+  } else if (!c.bnname.empty()) {
+    const float* bias = t.get(c.bnname, c.cout);
+    if (!bias) return EOSV_ERR_ARG;
+    for (int o = 0; o < c.cout; ++o) beta[o] = bias[o];
+  }
+  std::vector<float> wf((size_t)c.cout * c.K, 0.f);
+  for (int o = 0; o < c.cout; ++o)
+    for (int i = 0; i < c.cin; ++i)
+      for (int y = 0; y < c.kh; ++y)
+        for (int x = 0; x < c.kw; ++x) {
+          const float v = w[(((size_t)o * c.cin + i) * c.kh + y) * c.kw + x];
+          wf[(size_t)o * c.K + ((size_t)y * c.kwp + x) * c.cinp + i] = v * alpha[o];
+        }
+  int rc;
+  if (bf16) {
+    std::vector<unsigned short> wb(wf.size());
+    for (size_t i = 0; i < wf.size(); ++i) wb[i] = f2bf_host(wf[i]);
+    if ((rc = dmalloc(h, &c.w, wb.size() * 2))) return rc;
+    EOSV_HIP_CHECK(hipMemcpy(c.w, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+  } else {
+    if ((rc = dmalloc(h, &c.w, wf.size() * 4))) return rc;
+    EOSV_HIP_CHECK(hipMemcpy(c.w, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+  }
+  if ((rc = dmalloc(h, (void**)&c.b, (size_t)c.cout * 4))) return rc;
+  EOSV_HIP_CHECK(hipMemcpy(c.b, beta.data(), (size_t)c.cout * 4, hipMemcpyHostToDevice));
+  return EOSV_OK;
+}
+
+static hipEvent_t prof_event(eosv_handle* h) {
+  if (h->pool_used == h->pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    h->pool.push_back(e);
+  }
+  return h->pool[h->pool_used++];
+}
+
+static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, int W, const void* res,
+                    void* y, bool relu, bool bf16, hipStream_t s) {
+  ConvArgs a{};
+  a.x = x;
+  a.w = c.w;
+  a.bias = c.b;
+  a.res = res;
+  a.y = y;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.Cin = c.cinp;
+  a.Ho = conv_out(H, c.kh, c.stride, c.pad);
+  a.Wo = conv_out(W, c.kw, c.stride, c.pad);
+  a.Cout = c.cout;
+  a.KH = c.kh;
+  a.KW = c.kw;
+  a.KWp = c.kwp;
+  a.stride = c.stride;
+  a.pad = c.pad;
+  a.K = c.K;
+  a.relu = relu ? 1 : 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->prof) {
+    e0 = prof_event(h);
+    e1 = prof_event(h);
+    if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
+    EOSV_HIP_CHECK(hipEventRecord(e0, s));
+  }
+  const int rc = bf16 ? launch_conv_bf16(a, s) : launch_conv_f32(a, s);
+  if (h->prof && rc == EOSV_OK) {
+    EOSV_HIP_CHECK(hipEventRecord(e1, s));
+    const double macs = (double)N * a.Ho * a.Wo * c.cout * c.kh * c.kw * c.cin;
+    h->recs.push_back({c.id, e0, e1, 2.0 * macs});
+  }
+  return rc;
+}
+
+static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat, hipStream_t s) {
+  const bool bf = h->d.dtype == EOSV_BF16;
+  const int H = h->d.height, W = h->d.width;
+  int rc;
+  if ((rc = launch_pack_nchw_nhwc4(frames, B, H, W, h->pack, bf, s))) return rc;
+  if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, h->buf[0], true, bf, s))) return rc;
+  if ((rc = launch_maxpool3x3s2(h->buf[0], B, h->hs, h->ws, 64, h->buf[1], h->hp, h->wp, bf, s)))
+    return rc;
+  void* x = h->buf[1];
+  int hh = h->hp, ww = h->wp;
+  for (const Block& b : h->blocks) {
+    void* fr[3];
+    int nf = 0;
+    for (void* p : h->buf)
+      if (p != x) fr[nf++] = p;
+    const int st = b.bottleneck ? b.c2.stride : b.c1.stride;  // torchvision: stride on the 3x3
+    const int ho = conv_out(hh, 3, st, 1), wo = conv_out(ww, 3, st, 1);
+    void* r = x;
+    if (b.has_ds) {
+      r = fr[2];
+      if ((rc = run_conv(h, b.ds, x, B, hh, ww, nullptr, r, false, bf, s))) return rc;
+    }
+    if (!b.bottleneck) {
+      if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, r, r, true, bf, s))) return rc;
+    } else {
+      if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c2, fr[0], B, hh, ww, nullptr, fr[1], true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, r, r, true, bf, s))) return rc;
+    }
+    x = r;
+    hh = ho;
+    ww = wo;
+  }
+  return launch_avgpool(x, B, hh * ww, h->D, feat, bf, s);
+}
+
+}  // namespace eosv
+
+using namespace eosv;
+
+extern "C" {
+
+const char* eosv_last_error(void) { return g_err.c_str(); }
+
+int eosv_create(const eosv_desc* desc, eosv_handle** out) {
+  if (!desc || !out) {
+    set_error("eosv_create: null argument");
+    return EOSV_ERR_ARG;
+  }
+  *out = nullptr;
+  if (desc->height < 32 || desc->width < 32 || desc->max_frames <= 0 || desc->num_classes <= 0 ||
+      (desc->dtype != EOSV_F32 && desc->dtype != EOSV_BF16)) {
+    set_error("eosv_create: bad desc (height/width >= 32, max_frames > 0, dtype f32|bf16)");
+    return EOSV_ERR_ARG;
+  }
+  EOSV_HIP_CHECK(hipSetDevice(desc->device));
+  eosv_handle* h = new eosv_handle();
+  h->d = *desc;
+  int rc = build_plan(h);
+  const size_t elt = desc->dtype == EOSV_BF16 ? 2 : 4;
+  const size_t F = (size_t)desc->max_frames;
+  if (!rc) rc = dmalloc(h, &h->pack, F * desc->height * desc->width * 4 * elt);
+  for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);
+  if (rc) {
+    eosv_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return EOSV_OK;
+}
+
+int eosv_load_weights(eosv_handle* h, const char* const* names, const void* const* host_ptrs,
+                      const int64_t* numel, int n) {
+  if (!h || (n > 0 && (!names || !host_ptrs || !numel)) || n < 0) {
+    set_error("eosv_load_weights: bad argument");
+    return EOSV_ERR_ARG;
+  }
+  EOSV_HIP_CHECK(hipSetDevice(h->d.device));
+  Tensors t;
+  for (int i = 0; i < n; ++i) {
+    if (!names[i]) continue;
+    t.m[names[i]] = {(const float*)host_ptrs[i], numel[i]};
+  }
+  const bool bf = h->d.dtype == EOSV_BF16;
+  int rc;
+  h->loaded = false;
+  if ((rc = upload_conv(h, h->stem, t, bf, true))) return rc;
+  for (Block& b : h->blocks) {
+    if ((rc = upload_conv(h, b.c1, t, bf, true))) return rc;
+    if ((rc = upload_conv(h, b.c2, t, bf, true))) return rc;
+    if (b.bottleneck && (rc = upload_conv(h, b.c3, t, bf, true))) return rc;
+    if (b.has_ds && (rc = upload_conv(h, b.ds, t, bf, true))) return rc;
+  }
+  Conv& fc = h->fc;
+  fc.bnname = "fc.bias";
+  if ((rc = upload_conv(h, fc, t, false, false))) return rc;
+  h->loaded = true;
+  return EOSV_OK;
+}
+
+int eosv_backbone_forward(eosv_handle* h, const float* d_frames, int B, float* d_feat,
+                          eosv_stream_t stream) {
+  if (!h || B < 0 || (B > 0 && (!d_frames || !d_feat))) {
+    set_error("eosv_backbone_forward: bad argument");
+    return EOSV_ERR_ARG;
+  }
+  if (!h->loaded) {
+    set_error("eosv_backbone_forward: weights not loaded");
+    return EOSV_ERR_STATE;
+  }
+  const size_t fstride = (size_t)3 * h->d.height * h->d.width;
+  for (int b0 = 0; b0 < B; b0 += h->d.max_frames) {
+    const int nb = std::min(h->d.max_frames, B - b0);
+    int rc = forward_chunk(h, d_frames + b0 * fstride, nb, d_feat + (size_t)b0 * h->D,
+                           (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return EOSV_OK;
+}
+
+int eosv_fc_forward(eosv_handle* h, const float* d_feat, int B, float* d_logits, eosv_stream_t stream) {
+  if (!h || B < 0 || (B > 0 && (!d_feat || !d_logits))) {
+    set_error("eosv_fc_forward: bad argument");
+    return EOSV_ERR_ARG;
+  }
+  if (!h->loaded) {
+    set_error("eosv_fc_forward: weights not loaded");
+    return EOSV_ERR_STATE;
+  }
+  if (B == 0) return EOSV_OK;
+  return run_conv(h, h->fc, d_feat, B, 1, 1, nullptr, d_logits, false, false, (hipStream_t)stream);
+}
+
+int eosv_feature_dim(const eosv_handle* h) { return h ? h->D : EOSV_ERR_ARG; }
+
+int64_t eosv_device_bytes(const eosv_handle* h) { return h ? h->bytes : EOSV_ERR_ARG; }
+
+int eosv_profile_enable(eosv_handle* h, int enable) {
+  if (!h) return set_error("eosv_profile_enable: null handle"), EOSV_ERR_ARG;
+  h->prof = enable != 0;
+  h->recs.clear();
+  h->pool_used = 0;
+  return EOSV_OK;
+}
+
+int eosv_profile_read(eosv_handle* h, double* ms, double* flops, int64_t* launches, int max_layers) {
+  if (!h || max_layers < 0 || (max_layers > 0 && (!ms || !flops || !launches)))
+    return set_error("eosv_profile_read: bad argument"), EOSV_ERR_ARG;
+  for (int i = 0; i < max_layers; ++i) {
+    ms[i] = 0;
+    flops[i] = 0;
+    launches[i] = 0;
+  }
+  for (const auto& r : h->recs) {
+    EOSV_HIP_CHECK(hipEventSynchronize(r.b));
+    float t = 0;
+    EOSV_HIP_CHECK(hipEventElapsedTime(&t, r.a, r.b));
+    if (r.id < max_layers) {
+      ms[r.id] += t;
+      flops[r.id] += r.flops;
+      launches[r.id] += 1;
+    }
+  }
+  return h->n_layers;
+}
+
+void eosv_destroy(eosv_handle* h) {
+  if (!h) return;
+  for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
+  for (void* p : h->allocs) (void)hipFree(p);
+  delete h;
+}
+
+}  // extern "C"

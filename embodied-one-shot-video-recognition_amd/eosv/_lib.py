@@ -1,0 +1,91 @@
+"""ctypes binding of ``libeosv.so`` (the C ABI declared in include/eosv.h).
+
+There is no CPU fallback: if the library is missing or no HIP device is visible the
+calls raise.  The library is built in-tree (``csrc/Makefile`` or
+``__graft_entry__.build()``) next to this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libeosv.so")
+
+EOSV_F32, EOSV_BF16 = 0, 1
+MATCH_PROTONET, MATCH_COSINE = 0, 1
+MAX_COLS = 64
+
+_STATUS = {-1: "EOSV_ERR_ARG", -2: "EOSV_ERR_HIP", -3: "EOSV_ERR_OOM",
+           -4: "EOSV_ERR_UNSUPPORTED", -5: "EOSV_ERR_STATE"}
+
+# every symbol include/eosv.h declares
+EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_fc_forward",
+           "eosv_clip_embed", "eosv_segment_mean", "eosv_match", "eosv_segment_match",
+           "eosv_synth_frames", "eosv_profile_enable", "eosv_profile_read", "eosv_feature_dim", "eosv_device_bytes", "eosv_last_error",
+           "eosv_destroy")
+
+
+class EosvDesc(ctypes.Structure):
+    _fields_ = [("arch", ctypes.c_int), ("dtype", ctypes.c_int), ("height", ctypes.c_int),
+                ("width", ctypes.c_int), ("max_frames", ctypes.c_int), ("device", ctypes.c_int),
+                ("num_classes", ctypes.c_int)]
+
+
+class EosvError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libeosv.so once (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EosvError(f"{LIB_PATH} not built: run `make -C csrc` or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+    sig = {
+        "eosv_create": (i32, [ctypes.POINTER(EosvDesc), ctypes.POINTER(vp)]),
+        "eosv_load_weights": (i32, [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
+                                    ctypes.POINTER(i64), i32]),
+        "eosv_backbone_forward": (i32, [vp, vp, i32, vp, vp]),
+        "eosv_fc_forward": (i32, [vp, vp, i32, vp, vp]),
+        "eosv_clip_embed": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
+        "eosv_segment_mean": (i32, [vp, i32, i32, i32, vp, vp]),
+        "eosv_match": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp]),
+        "eosv_segment_match": (i32, [vp, i32, vp, i32, i32, f32, f32, vp, vp, vp]),
+        "eosv_synth_frames": (i32, [vp, i32, i32, i32, vp, vp]),
+        "eosv_profile_enable": (i32, [vp, i32]),
+        "eosv_profile_read": (i32, [vp, vp, vp, vp, i32]),
+        "eosv_feature_dim": (i32, [vp]),
+        "eosv_device_bytes": (i64, [vp]),
+        "eosv_last_error": (ctypes.c_char_p, []),
+        "eosv_destroy": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().eosv_last_error().decode(errors="replace")
+        raise EosvError(f"{what} failed: {_STATUS.get(rc, rc)}: {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

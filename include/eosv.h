@@ -1,0 +1,139 @@
+/*
+ * eosv.h -- C ABI of the MI355X-native clip-embedding + one-shot matching path.
+ *
+ * The reference (lovelyqian/Embodied-One-Shot-Video-Recognition) is pure Python with
+ * no FFI; its hot path is implicit torch/cuDNN work behind three Python call sites.
+ * Each entry point below replaces one of them (reference file:line in the comment);
+ * the Python drop-in modules (models.py, network_test.py, classifier.py, ...) bind
+ * these with ctypes.
+ *
+ * Conventions:
+ *   - every function returns 0 (EOSV_OK) or a negative eosv_status; a thread-local
+ *     message is available from eosv_last_error().  No exception crosses the ABI.
+ *   - all d_* pointers are DEVICE pointers owned by the caller; nothing is freed
+ *     across the boundary.  The library owns weights + workspace inside the handle.
+ *   - calls enqueue on the given stream (a hipStream_t; NULL = default stream) and do
+ *     not synchronise.  A handle is bound to one device and is not re-entrant.
+ */
+#ifndef EOSV_H
+#define EOSV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* eosv_stream_t; /* == hipStream_t */
+typedef struct eosv_handle eosv_handle;
+
+typedef enum {
+  EOSV_OK = 0,
+  EOSV_ERR_ARG = -1,         /* bad argument / shape / missing tensor */
+  EOSV_ERR_HIP = -2,         /* a HIP runtime call failed */
+  EOSV_ERR_OOM = -3,         /* device allocation failed */
+  EOSV_ERR_UNSUPPORTED = -4, /* arch / dtype / shape not implemented */
+  EOSV_ERR_STATE = -5        /* e.g. forward before eosv_load_weights */
+} eosv_status;
+
+typedef enum { EOSV_ARCH_R18 = 18, EOSV_ARCH_R50 = 50, EOSV_ARCH_R101 = 101 } eosv_arch;
+typedef enum { EOSV_F32 = 0, EOSV_BF16 = 1 } eosv_dtype;
+typedef enum { EOSV_MATCH_PROTONET = 0, EOSV_MATCH_COSINE = 1 } eosv_match_kind;
+
+typedef struct {
+  int arch;        /* eosv_arch */
+  int dtype;       /* eosv_dtype: arithmetic of the conv stack (f32 = exact-f32 MFMA) */
+  int height;      /* frame height (224, 256, ...) */
+  int width;
+  int max_frames;  /* frames per internal chunk; workspace is sized for this */
+  int device;      /* HIP device ordinal */
+  int num_classes; /* fc output size (reference: num_classes_train = 64) */
+} eosv_desc;
+
+/* Create a handle (allocates workspace).  Replaces the construction at
+ * reference models.py:9-16 / 24-31 (torchvision resnet18/50 + fc). */
+int eosv_create(const eosv_desc* desc, eosv_handle** out);
+
+/* Upload a state_dict (reference keys, models.py:14-16: convnet.{0,1,4..7}.*, fc.*).
+ * host_ptrs[i] points to numel[i] float32 values (num_batches_tracked entries are
+ * ignored and may be NULL).  BN is folded into the conv weights here.
+ * Replaces load_state_dict(torch.load(pkl)) at network_test.py:133-135. */
+int eosv_load_weights(eosv_handle* h, const char* const* names, const void* const* host_ptrs,
+                      const int64_t* numel, int n);
+
+/* Backbone forward: d_frames [B,3,H,W] float32 NCHW (post-Normalize) ->
+ * d_feat [B,D] float32 (D = 512 for R18, 2048 for R50/R101) = convnet(x).view(B,-1).
+ * Replaces self.convnet(x) at models.py:19-20 / 34-35. */
+int eosv_backbone_forward(eosv_handle* h, const float* d_frames, int B, float* d_feat,
+                          eosv_stream_t stream);
+
+/* fc head: d_feat [B,D] -> d_logits [B,num_classes].  models.py:21 / 36. */
+int eosv_fc_forward(eosv_handle* h, const float* d_feat, int B, float* d_logits,
+                    eosv_stream_t stream);
+
+/* Clip embedding: for clip c, frames d_feat[offsets[c] .. offsets[c]+counts[c]) are
+ * (optionally) L2-normalised (F.normalize p=2, eps 1e-12) and averaged with a
+ * sequential f32 sum / count.  d_offsets/d_counts are device int32 [n_clips].
+ * Replaces network_test.py:62-65 (and :79-80 with counts == 1). */
+int eosv_clip_embed(const float* d_feat, const int32_t* d_offsets, const int32_t* d_counts,
+                    int n_clips, int D, int l2, float* d_emb, eosv_stream_t stream);
+
+/* Segment mean: d_feat [n_seg*seg_len, D] -> d_seg [n_seg, D] = mean over seg_len
+ * consecutive rows.  network_test.py:188-189, 204-205. */
+int eosv_segment_mean(const float* d_feat, int n_seg, int seg_len, int D, float* d_seg,
+                      eosv_stream_t stream);
+
+/* One-shot matching of n_episodes episodes in one launch.
+ *   d_query    [n_episodes, D]      query clip embedding of each episode
+ *   d_support  [sum S_e, D]         support embeddings, episode e at rows sup_off[e]..
+ *   d_sup_off  [n_episodes+1]       int32 row offsets into d_support
+ *   d_sup_slot [sum S_e]            int32 prototype slot of each support row
+ *                                   (first-appearance order of its label, classifier.py:20-36)
+ *   d_n_proto  [n_episodes]         int32 prototypes per episode (<= 64)
+ * kind = PROTONET: f64 cdist to per-slot means -> f32 -> softmax(-d) -> argmax
+ *        (classifier.py:43-90); d_pred = prototype position, d_score = distances.
+ * kind = COSINE:   cosine similarity to every support row -> argmax (classifier.py:117-120);
+ *        d_pred = support row index within the episode, d_score = similarities.
+ * d_score [n_episodes, max_cols] f32 (may be NULL), max_cols = 64. */
+int eosv_match(const float* d_query, const float* d_support, const int32_t* d_sup_off,
+               const int32_t* d_sup_slot, const int32_t* d_n_proto, int n_episodes, int D,
+               int kind, int64_t* d_pred, float* d_score, eosv_stream_t stream);
+
+/* Config-3 gallery matching (network_test.py:207-214 + models.py:42-56):
+ * dist = cdist(d_seg [S,D], d_gallery [G,D]) in f64 -> f32 -> 3-tap smoothing
+ * [l1,l2,l1] along the S axis with zero padding -> first argmin over G per row.
+ * d_ids [S] int64; d_dist [S,G] f32 smoothed distances (may be NULL). */
+int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G, int D,
+                       float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
+                       eosv_stream_t stream);
+
+/* Deterministic synthetic frames, bit-identical to eosv/synth.py:synth_frame.
+ * For frame f: class seed, video seed, noise seed (u64) and frame id in d_params
+ * [n_frames, 4] (u64); writes d_frames [n_frames,3,H,W] f32 NCHW.  Frames with
+ * frame id 0 are written as zeros (the reference's zero padding, utils.py:250-253). */
+int eosv_synth_frames(const uint64_t* d_params, int n_frames, int H, int W, float* d_frames,
+                      eosv_stream_t stream);
+
+/* Kernel timing for the roofline report: while enabled, every conv launch of the
+ * handle is bracketed by HIP events on its stream (layer id = position in the plan:
+ * 0 = stem, then each block's convs in order, fc last).  eosv_profile_read
+ * synchronises on the recorded events and returns, per layer id < max_layers,
+ * the summed milliseconds, summed algorithmic FLOPs (2 x MACs) and launch count;
+ * the return value is the number of layer ids in the plan.  Enabling clears the log. */
+int eosv_profile_enable(eosv_handle* h, int enable);
+int eosv_profile_read(eosv_handle* h, double* ms, double* flops, int64_t* launches, int max_layers);
+
+/* Feature dimension D of the handle's backbone. */
+int eosv_feature_dim(const eosv_handle* h);
+
+/* Device bytes held by the handle (weights + workspace). */
+int64_t eosv_device_bytes(const eosv_handle* h);
+
+const char* eosv_last_error(void);
+void eosv_destroy(eosv_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EOSV_H */

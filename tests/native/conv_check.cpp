@@ -1,0 +1,79 @@
+// Layer-level check of the implicit-GEMM conv against a naive CPU conv (double accum).
+// Build: hipcc --offload-arch=gfx950 -O2 -I include -I <pkg>/csrc conv_check.cpp -L<pkg> -leosv
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "common.h"
+
+using namespace eosv;
+
+static float frand(unsigned& s) { s = s * 1664525u + 1013904223u; return ((s >> 8) & 0xffff) / 32768.f - 1.f; }
+
+static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int pad, bool stem, bool res, bool relu) {
+  const int KWp = stem ? 8 : K, Cinp = stem ? 4 : Cin;
+  const int Ho = (H + 2 * pad - K) / stride + 1, Wo = (W + 2 * pad - K) / stride + 1;
+  const int Kd = K * KWp * Cinp;
+  unsigned s = 12345;
+  std::vector<float> x((size_t)N * H * W * Cinp), w((size_t)Cout * Kd, 0.f), b(Cout), r((size_t)N * Ho * Wo * Cout);
+  for (size_t i = 0; i < x.size(); ++i) x[i] = (stem && (i % 4 == 3)) ? 0.f : frand(s);
+  for (int o = 0; o < Cout; ++o)
+    for (int kh = 0; kh < K; ++kh)
+      for (int kw = 0; kw < K; ++kw)
+        for (int c = 0; c < Cin; ++c) w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c] = frand(s);
+  for (auto& v : b) v = frand(s);
+  for (auto& v : r) v = frand(s);
+  float *dx, *dw, *db, *dr, *dy;
+  hipMalloc(&dx, x.size() * 4); hipMalloc(&dw, w.size() * 4); hipMalloc(&db, b.size() * 4);
+  hipMalloc(&dr, r.size() * 4); hipMalloc(&dy, r.size() * 4);
+  hipMemcpy(dx, x.data(), x.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dw, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db, b.data(), b.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dr, r.data(), r.size() * 4, hipMemcpyHostToDevice);
+  ConvArgs a{};
+  a.x = dx; a.w = dw; a.bias = db; a.res = res ? dr : nullptr; a.y = dy;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cinp; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.KH = K; a.KW = K; a.KWp = KWp; a.stride = stride; a.pad = pad; a.K = Kd; a.relu = relu;
+  int rc = launch_conv_f32(a, 0);
+  hipDeviceSynchronize();
+  std::vector<float> y(r.size());
+  hipMemcpy(y.data(), dy, y.size() * 4, hipMemcpyDeviceToHost);
+  double maxerr = 0, maxref = 0; long bad = 0;
+  for (int n = 0; n < N; ++n)
+    for (int oh = 0; oh < Ho; ++oh)
+      for (int ow = 0; ow < Wo; ++ow)
+        for (int o = 0; o < Cout; ++o) {
+          double acc = b[o];
+          for (int kh = 0; kh < K; ++kh)
+            for (int kw = 0; kw < K; ++kw) {
+              int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+              if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+              for (int c = 0; c < Cin; ++c)
+                acc += (double)x[(((size_t)n * H + ih) * W + iw) * Cinp + c] * w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c];
+            }
+          size_t oi = (((size_t)n * Ho + oh) * Wo + ow) * Cout + o;
+          if (res) acc += r[oi];
+          if (relu && acc < 0) acc = 0;
+          double e = fabs(acc - y[oi]);
+          if (e > 1e-3 * (1 + fabs(acc))) { if (bad < 5) printf("  bad n%d oh%d ow%d o%d ref %f got %f\n", n, oh, ow, o, acc, y[oi]); ++bad; }
+          maxerr = fmax(maxerr, e); maxref = fmax(maxref, fabs(acc));
+        }
+  printf("%s N%d H%d W%d Cin%d Cout%d K%d s%d p%d res%d relu%d rc=%d maxerr %.3e (maxref %.3e) bad %ld\n",
+         bad ? "FAIL" : "ok  ", N, H, W, Cin, Cout, K, stride, pad, res, relu, rc, maxerr, maxref, bad);
+  hipFree(dx); hipFree(dw); hipFree(db); hipFree(dr); hipFree(dy);
+  return bad ? 1 : 0;
+}
+
+int main() {
+  int fails = 0;
+  fails += check(1, 8, 8, 32, 64, 1, 1, 0, false, false, false);
+  fails += check(2, 9, 7, 64, 64, 3, 1, 1, false, false, false);
+  fails += check(2, 14, 14, 64, 128, 3, 2, 1, false, true, true);
+  fails += check(3, 7, 7, 256, 512, 1, 2, 0, false, false, false);
+  fails += check(1, 7, 7, 512, 512, 3, 1, 1, false, true, true);
+  fails += check(2, 30, 30, 3, 64, 7, 2, 3, true, false, true);
+  fails += check(5, 1, 1, 512, 64, 1, 1, 0, false, false, false);
+  printf("%d failures\n", fails);
+  return fails;
+}

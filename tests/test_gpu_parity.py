@@ -1,0 +1,133 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden
+vectors captured from the reference.
+
+Tolerances (north star): integer predictions bit-exact; f32 embeddings within 1e-4
+relative (asserted as max|gpu-ref| <= 1e-4 * max|ref| per clip).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _common import load_fixture, load_video
+from eosv import arch, engine, synth
+from oracle import harness_ref, resnet_ref
+
+pytestmark = pytest.mark.gpu
+
+EMB_RTOL = 1e-4
+
+
+def _rel_err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+@pytest.fixture(scope="module")
+def r18():
+    bb = engine.Backbone("resnet18", "f32", 224, 224, max_frames=128)
+    bb.load_state_dict(synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0))
+    yield bb
+    bb.close()
+
+
+@pytest.fixture(scope="module")
+def oracle_r18():
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    return resnet_ref.build_model("resnet18", synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0))
+
+
+def test_synth_frames_bit_exact():
+    eps = [dict(support=["bowling/abc_000001_000011"], support_y=[0], query="bowling/xyz_000002_000012", query_y=0)]
+    b = engine.build_episode_batch(eps, T=16)
+    for H, W in ((224, 224), (97, 61)):
+        dev = engine.synth_frames(b.params, H, W).cpu().numpy()
+        k = 0
+        for vi in ("bowling/abc_000001_000011", "bowling/xyz_000002_000012"):
+            for f in engine.video_frames(vi, 16):
+                ref = synth.synth_frame("bowling", vi, f, H, W)
+                assert np.array_equal(dev[k].view(np.uint32), ref.view(np.uint32)), (H, W, vi, f)
+                k += 1
+
+
+@pytest.mark.parametrize("B", [1, 7, 33])
+def test_backbone_features_r18(r18, oracle_r18, B):
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 3, 224, 224, generator=g)
+    with torch.no_grad():
+        ref, ref_logits = oracle_r18(x)
+    out = r18.forward(x.cuda()).cpu()
+    assert _rel_err(out.numpy(), ref.numpy()) < 1e-5
+    logits = r18.fc(out.cuda()).cpu()
+    assert _rel_err(logits.numpy(), ref_logits.numpy()) < 1e-5
+
+
+def test_clip_embed_matches_reference_order():
+    g = torch.Generator().manual_seed(0)
+    feat = torch.rand(40, 512, generator=g) * 3
+    counts = np.array([16, 1, 7, 16], np.int32)
+    offs = np.array([0, 16, 17, 24], np.int32)
+    emb = engine.clip_embed(feat.cuda(), torch.from_numpy(offs).cuda(), torch.from_numpy(counts).cuda()).cpu()
+    for c in range(4):
+        f = feat[offs[c]:offs[c] + counts[c]]
+        ref = np.mean(torch.nn.functional.normalize(f, p=2, dim=1).numpy(), axis=0)
+        np.testing.assert_allclose(emb[c].numpy(), ref, rtol=2e-6, atol=1e-8)
+    raw = engine.clip_embed(feat.cuda(), torch.from_numpy(offs).cuda(), torch.from_numpy(counts).cuda(), l2=False).cpu()
+    np.testing.assert_allclose(raw[0].numpy(), np.mean(feat[:16].numpy(), axis=0), rtol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["protonet", "cosine"])
+def test_match_kernel_vs_oracle(kind):
+    rng = np.random.default_rng(1)
+    E, D = 50, 512
+    eps_sup, off, slots, nproto, q = [], [0], [], [], []
+    for e in range(E):
+        k = 1 + e % 3
+        n = 5
+        ys = np.repeat(np.arange(n), k).astype(np.float32)
+        s = rng.random((n * k, D), dtype=np.float32)
+        eps_sup.append((s, ys))
+        off.append(off[-1] + n * k)
+        slots += [int(y) for y in ys]
+        nproto.append(n)
+        q.append(rng.random(D, dtype=np.float32))
+    sup = torch.from_numpy(np.concatenate([s for s, _ in eps_sup])).cuda()
+    qt = torch.from_numpy(np.stack(q)).cuda()
+    t = lambda a: torch.from_numpy(np.array(a, np.int32)).cuda()  # noqa: E731
+    pred, score = engine.match(qt, sup, t(off), t(slots), t(nproto), kind)
+    pred = pred.cpu().numpy()
+    for e, (s, ys) in enumerate(eps_sup):
+        qq = q[e][None]
+        if kind == "protonet":
+            rp, rd = harness_ref.protonet_predict(s, ys, qq, np.array([0.0]))
+            np.testing.assert_allclose(score[e, :5].cpu().numpy(), rd[0], rtol=1e-6)
+        else:
+            rp, _ = harness_ref.cosine_predict(s, qq)
+        assert pred[e] == rp[0], (e, kind)
+
+
+def test_segment_match_vs_oracle():
+    rng = np.random.default_rng(2)
+    S, G, D = 40, 700, 256
+    seg = rng.random((S, D), dtype=np.float32)
+    gal = rng.random((G, D), dtype=np.float32)
+    ids, dist = engine.segment_match(torch.from_numpy(seg).cuda(), torch.from_numpy(gal).cuda(), 0.1, 1.0)
+    from scipy.spatial.distance import cdist
+    ref = harness_ref.temporal_smooth(cdist(seg, gal, "euclidean"))
+    np.testing.assert_allclose(dist.cpu().numpy(), ref, rtol=1e-6)
+    assert np.array_equal(ids.cpu().numpy(), np.argsort(ref, axis=1)[:, 0])
+
+
+def test_golden_c1_r18_episodes(r18):
+    """Config 1 fixture (20 reference episodes) through the batched device path."""
+    meta, arr = load_fixture("c1_r18_protonet_seed1")
+    b = engine.build_episode_batch(meta["episodes"], T=16)
+    dev = engine.DeviceEpisodes(b, 224, 224)
+    pred, emb, _ = engine.run_episodes(r18, dev, "protonet", True)
+    emb = emb.cpu().numpy()
+    E = len(meta["episodes"])
+    sup = emb[:b.n_support].reshape(E, 5, -1)
+    qry = emb[b.n_support:]
+    for e in range(E):
+        assert _rel_err(sup[e], arr["support_feature"][e]) < EMB_RTOL
+        assert _rel_err(qry[e], arr["query_feature"][e][0]) < EMB_RTOL
+    assert np.array_equal(pred.cpu().numpy(), arr["pred"][:, 0])
