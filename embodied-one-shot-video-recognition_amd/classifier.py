@@ -1,0 +1,71 @@
+"""Drop-in for the reference's ``classifier.py`` (lines 9-123), matching on the GPU.
+
+``Classifier(kind).predict(data_result)`` takes the same dict (support_feature [S,D],
+support_y [S], query_feature [Q,D], query_y [Q]; numpy or torch) and returns a numpy
+int64 [Q] array with the reference's meaning:
+  * 'protonet': position of the nearest prototype, prototypes in first-appearance
+    order of the labels (classifier.py:9-90: f64 cdist -> f32 -> softmax(-d) -> argmax);
+  * 'cosine'  : index of the most similar SUPPORT row (classifier.py:117-120).
+Both run in the eosv match kernel.  The reference's protonet accepts exactly one
+query (classifier.py:58 shadows ``query_feature``; Q>1 raises IndexError); here each
+of Q queries is matched against the same support set.  'SVM' / 'KNN' (sklearn, not on
+the north-star path; KNN is broken in the reference) are not provided.
+"""
+import numpy as np
+import torch
+
+from eosv import engine as _engine
+
+
+def _np(a):
+    return a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+
+
+def generate_prototypes_tensor_lowerdim(data):
+    """classifier.py:9-40: (prototype_ids, prototype_features) in first-appearance order."""
+    support_feature, support_y = _np(data['support_feature']), _np(data['support_y'])
+    groups = {}
+    for i in range(support_y.shape[0]):
+        groups.setdefault(support_y[i], []).append(support_feature[i])
+    ids = list(groups.keys())
+    feats = np.array([np.mean(np.array(groups[c]), axis=0) for c in ids])
+    return ids, feats
+
+
+def _match(data, kind):
+    sup = np.ascontiguousarray(_np(data['support_feature']), dtype=np.float32)
+    qry = np.ascontiguousarray(_np(data['query_feature']), dtype=np.float32).reshape(-1, sup.shape[1])
+    sy = _np(data['support_y']).reshape(-1)
+    Q, S = qry.shape[0], sup.shape[0]
+    slots, seen = [], {}
+    for y in sy:
+        slots.append(seen.setdefault(y.item() if hasattr(y, 'item') else y, len(seen)))
+    if len(seen) > _engine.MAX_COLS:
+        raise ValueError(f"at most {_engine.MAX_COLS} prototypes per episode")
+    dev = torch.device('cuda', torch.cuda.current_device())
+    sup_t = torch.from_numpy(np.tile(sup, (Q, 1))).to(dev)
+    t = lambda a: torch.from_numpy(np.asarray(a, np.int32)).to(dev)  # noqa: E731
+    pred, score = _engine.match(torch.from_numpy(qry).to(dev), sup_t, t(np.arange(Q + 1) * S),
+                                t(np.tile(slots, Q)), t([len(seen)] * Q), kind)
+    return pred.cpu().numpy().astype(np.int64), score.cpu().numpy()
+
+
+def one_shot_classifier_prototype_lowerdim(data):
+    """classifier.py:43-90 -> predicted_y (prototype positions)."""
+    return _match(data, 'protonet')[0]
+
+
+class Classifier():
+    def __init__(self, classifier='protonet'):
+        self.classifier = classifier
+
+    def predict(self, data_result):
+        if self.classifier == 'protonet':
+            return one_shot_classifier_prototype_lowerdim(data_result)
+        if self.classifier == 'cosine':
+            return _match(data_result, 'cosine')[0]
+        if self.classifier in ('SVM', 'KNN'):
+            raise NotImplementedError(f"classifier '{self.classifier}' is outside the GPU path "
+                                      "(sklearn; not part of the north-star scope)")
+        print('classifier type error.')
+        return None

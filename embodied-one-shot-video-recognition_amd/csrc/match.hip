@@ -250,9 +250,33 @@ __global__ __launch_bounds__(256) void seg_smooth_argmin_kernel(const float* __r
   }
 }
 
+__global__ void temporal_smooth_kernel(const float* __restrict__ x, int rows, int cols, float l1, float l2,
+                                       float* __restrict__ y) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)rows * cols) return;
+  const int c = (int)(t % cols);
+  const float xm = c > 0 ? x[t - 1] : 0.f;
+  const float xp = c + 1 < cols ? x[t + 1] : 0.f;
+  y[t] = fmaf(l1, xp, fmaf(l2, x[t], l1 * xm));
+}
+
 }  // namespace eosv
 
 using namespace eosv;
+
+extern "C" int eosv_temporal_smooth(const float* d_x, int rows, int cols, float lamda1, float lamda2, float* d_y,
+                                    eosv_stream_t stream) {
+  if (rows < 0 || cols < 0 || ((long long)rows * cols > 0 && (!d_x || !d_y)) || d_x == d_y) {
+    set_error("eosv_temporal_smooth: bad argument (in-place not supported)");
+    return EOSV_ERR_ARG;
+  }
+  const long long total = (long long)rows * cols;
+  if (total == 0) return EOSV_OK;
+  hipLaunchKernelGGL(temporal_smooth_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, d_x, rows, cols, lamda1, lamda2, d_y);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
 
 extern "C" int eosv_match(const float* d_query, const float* d_support, const int32_t* d_sup_off,
                           const int32_t* d_sup_slot, const int32_t* d_n_proto, int n_episodes, int D,

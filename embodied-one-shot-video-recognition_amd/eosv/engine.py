@@ -187,6 +187,17 @@ def segment_match(seg: torch.Tensor, gallery: torch.Tensor, lamda1: float, lamda
     return ids, dist
 
 
+def temporal_smooth(x: torch.Tensor, lamda1: float, lamda2: float, stream=None) -> torch.Tensor:
+    """3-tap [l1,l2,l1] smoothing along the last axis, zero padded (models.py:42-56)."""
+    _require_cuda(x, "x", torch.float32)
+    cols = x.shape[-1] if x.dim() else 1
+    rows = x.numel() // max(cols, 1)
+    y = torch.empty_like(x)
+    check(lib().eosv_temporal_smooth(ptr(x), rows, cols, float(lamda1), float(lamda2), ptr(y), stream_ptr(stream)),
+          "eosv_temporal_smooth")
+    return y
+
+
 def synth_frames(params: np.ndarray, H: int, W: int, device=None, out: Optional[torch.Tensor] = None,
                  stream=None) -> torch.Tensor:
     """Generate frames [F,3,H,W] on the device from a [F,4] u64 table (see frame_table)."""

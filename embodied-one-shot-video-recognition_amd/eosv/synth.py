@@ -99,14 +99,31 @@ def noise_seed(video_info: str, fid: int) -> int:
     return mix64_int(((crc32(video_info) << 20) + fid) ^ TAG_NOISE)
 
 
+_TRAIN_CLASSES = None
+
+
+def _train_classes():
+    global _TRAIN_CLASSES
+    if _TRAIN_CLASSES is None:
+        import os
+
+        p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sources/data/train.list")
+        with open(p) as f:
+            _TRAIN_CLASSES = frozenset(line.split("/")[0] for line in f if line.strip())
+    return _TRAIN_CLASSES
+
+
 def frame_count(video_info: str) -> int:
     """Number of JPEG frames the synthetic video has (``len(listdir) - 1``, utils.py:103).
 
-    1 in 16 videos is short (4..15 frames) so that the reference's zero-padding and
-    truncation paths (utils.py:105-112, 249-257; network_test.py:54-55) are exercised.
+    1 in 16 videos of the novel (non-train) classes is short (4..15 frames) so that the
+    reference's zero-padding and truncation paths (utils.py:105-112, 249-257;
+    network_test.py:54-55) are exercised.  Train-split videos are never short: the
+    reference's gallery loader (generate_augmented_datasets.py:25-36) stacks them and
+    needs full 16-frame clips, as the real miniKinetics videos provide.
     """
     h = crc32(video_info)
-    if h % 16 == 0:
+    if h % 16 == 0 and video_info.split("/")[0] not in _train_classes():
         return 4 + (h >> 8) % 12
     return 250 + h % 51
 

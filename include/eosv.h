@@ -107,6 +107,11 @@ int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G,
                        float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
                        eosv_stream_t stream);
 
+/* TemporalLayer (models.py:42-56, PyTorch-1.x conv semantics): y[r][c] = l1*x[r][c-1]
+ * + l2*x[r][c] + l1*x[r][c+1] along the last axis, zero padded; d_x/d_y [rows, cols]. */
+int eosv_temporal_smooth(const float* d_x, int rows, int cols, float lamda1, float lamda2,
+                         float* d_y, eosv_stream_t stream);
+
 /* Deterministic synthetic frames, bit-identical to eosv/synth.py:synth_frame.
  * For frame f: class seed, video seed, noise seed (u64) and frame id in d_params
  * [n_frames, 4] (u64); writes d_frames [n_frames,3,H,W] f32 NCHW.  Frames with
