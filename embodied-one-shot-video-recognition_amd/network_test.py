@@ -276,7 +276,7 @@ class TestNetwork():
         preds = []
         B = max(1, self.episodes_per_batch // 8)
         for b0 in range(0, len(mine), B):
-            preds += self._aug_batch([plans[e] for e in mine[b0:b0 + B]], gal)
+            preds += self._aug_batch([plans[e] for e in mine[b0:b0 + B]], gal, getattr(self, 'debug', None))
         accs, _ = self._gather(mine, preds, n, [p['query_y'] for p in plans])
         self.last_accs = accs
         if rank == 0:

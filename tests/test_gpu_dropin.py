@@ -113,3 +113,40 @@ def test_temporal_layer_dropin():
     np.testing.assert_allclose(got, ref, rtol=1e-6)
     y = models.TemporalLayer()(torch.from_numpy(dist.T.astype(np.float32)).cuda().view(1, 1, 5120, 40))
     assert y.shape == (1, 1, 5120, 40)
+
+
+def test_aug_segment_reproduces_reference(tmp_path):
+    """Config-3 path (R50, aug_seg_T) against the reference's own run (2 episodes)."""
+    import generate_augmented_datasets as gad
+    import network_test
+    import utils
+
+    meta, arr = load_fixture("c3_r50_aug_seed4")
+    pkl = str(tmp_path / "model.pkl")
+    _save_sd("resnet50", pkl)
+    old = (utils.GALLERY_LIST, utils.EPISODE_NUMS["test"])
+    utils.GALLERY_LIST = str(tmp_path / "gallery.list")
+    utils.EPISODE_NUMS["test"] = len(meta["episodes"])
+    try:
+        random.seed(meta["seed"])
+        np.random.seed(meta["seed"])
+        gad.generate_gallery_list()
+        assert gad.gallery_video_infos() == meta["gallery"]
+        acc_path = str(tmp_path / "acc.txt")
+        tn = network_test.TestNetwork(acc_path, "resnet50", "protonet", True)
+        tn.debug = {}
+        tn.test_network_aug_segment(pre_model=pkl)
+        tn.acc_file.close()
+    finally:
+        utils.GALLERY_LIST, utils.EPISODE_NUMS["test"] = old
+    dbg = tn.debug
+    ref_pool = np.argsort(arr["smoothed"], axis=2)[:, :, 0]  # [E,40] (network_test.py:211-212)
+    got_pool = dbg["pool"].cpu().numpy().reshape(len(meta["episodes"]), -1)
+    assert np.array_equal(got_pool, ref_pool)
+    sup = dbg["sup"].cpu().numpy().reshape(arr["aug_features"].shape)
+    err = np.abs(sup - arr["aug_features"]).max() / np.abs(arr["aug_features"]).max()
+    assert err < 1e-4, err
+    q = dbg["q_emb"].cpu().numpy()
+    assert np.abs(q - arr["query_feature"][:, 0]).max() / np.abs(arr["query_feature"]).max() < 1e-4
+    assert np.array_equal(dbg["pred"].cpu().numpy(), arr["pred"][:, 0])
+    assert open(acc_path).read() == meta["acc_file"]
