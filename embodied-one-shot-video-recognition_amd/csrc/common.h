@@ -42,9 +42,12 @@ struct ConvArgs {
   int KH, KW, KWp, stride, pad;
   int K;              // padded reduction length, multiple of the kernel's BK
   int relu;
+  const void* zero;   // >= 64 zeroed bytes (DMA target for out-of-bounds taps)
+  int abl;            // ablation bits for profiling builds (0 = normal)
 };
 
 int launch_conv_f32(const ConvArgs& a, hipStream_t s);
+int launch_conv_f32_dma(const ConvArgs& a, hipStream_t s, int variant);
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ layout / pooling

@@ -178,16 +178,21 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(ConvArgs a) {
 }
 
 template <int BM, int BN, bool STEM>
-static int launch_tile(const ConvArgs& a, hipStream_t s) {
+static int launch_v1(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
-  if (nb > 0x7fffffffLL) {
-    set_error("conv: grid too large");
-    return EOSV_ERR_UNSUPPORTED;
-  }
+  if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((conv_f32_kernel<BM, BN, STEM>), dim3((unsigned)nb), dim3(256), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
+}
+
+static int conv_impl() {
+  static int v = [] {
+    const char* e = getenv("EOSV_CONV_IMPL");
+    return e ? atoi(e) : 5;
+  }();
+  return v;
 }
 
 int launch_conv_f32(const ConvArgs& a, hipStream_t s) {
@@ -196,9 +201,13 @@ int launch_conv_f32(const ConvArgs& a, hipStream_t s) {
     set_error("conv_f32: unsupported shape (K % 32, Cin % 32 or stem layout)");
     return EOSV_ERR_UNSUPPORTED;
   }
-  if (stem) return launch_tile<128, 64, true>(a, s);
-  if (a.Cout <= 64) return launch_tile<128, 64, false>(a, s);
-  return launch_tile<128, 128, false>(a, s);
+  const int impl = a.zero ? conv_impl() : 1;
+  if (impl == 1) {
+    if (stem) return launch_v1<128, 64, true>(a, s);
+    if (a.Cout <= 64) return launch_v1<128, 64, false>(a, s);
+    return launch_v1<128, 128, false>(a, s);
+  }
+  return launch_conv_f32_dma(a, s, impl);
 }
 
 }  // namespace eosv

@@ -1,0 +1,236 @@
+// Implicit-GEMM conv, exact-f32 MFMA, LDS-DMA staging (v2 of conv_f32.hip).
+//
+// Same GEMM view as conv_f32.hip (M = N*Ho*Wo, N = Cout, K = taps x Cin, B = [Cout][K]),
+// but the A/B tiles move HBM/L2 -> LDS with global_load_lds_dwordx4 into a 2-deep LDS
+// ring: no staging registers, ONE barrier per K-step, the next tile's DMA in flight
+// while the current one feeds the MFMAs.
+//
+// LDS image: each DMA wave-instruction writes 1 KiB linearly (lane*16 B), i.e. 1024/(4*BK)
+// whole rows, so rows are unpadded.  Bank spread comes from an XOR swizzle applied on
+// the SOURCE address: physical 16-B chunk c' of row r holds logical chunk c' ^ f(r),
+// f(r) = (r / (64/BK)) & (BK/4 - 1).  For the MFMA fragment reads (lane -> row lane&31,
+// chunk h*BK/8 + g) every ds_read_b128 lane group then touches 16 distinct bank slots.
+// Out-of-bounds im2col taps (zero padding, M/N tails) read a zeroed 16-B line (a.zero).
+//
+// Addressing is hoisted: each lane keeps, per staged row, the pointer of its (ih0, iw0)
+// pixel and the validity window; per K-step only a wave-uniform tap offset is added.
+#include "common.h"
+
+namespace eosv {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int CPR = BK / 4;         // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;       // rows per DMA instruction
+  constexpr int RPB = 64 / BK;        // rows per 256-B bank row
+  constexpr int AI = BM / (RPI * NW);  // DMA instructions per wave (A)
+  constexpr int BI = BN / (RPI * NW);
+  constexpr int STAGE = (BM + BN) * BK;
+  static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile shape");
+  static_assert(!STEM || BK == 32, "stem needs one kernel row per K-step");
+  __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
+  static_assert(NS == 2 || NS == 3, "ring depth");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int HoWo = a.Ho * a.Wo;
+  const int M = a.N * HoWo;
+  const int nN = (a.Cout + BN - 1) / BN;
+  const int mt = blockIdx.x / nN;
+  const int nt = blockIdx.x - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const float* __restrict__ x = (const float*)a.x;
+  const float* __restrict__ w = (const float*)a.w;
+  const float* zero = (const float*)a.zero;
+
+  const int lr = lane / CPR;
+  const int pc = lane % CPR;
+  // per staged A row: pointer at pixel (ih0, iw0) + this lane's logical chunk, and ih0/iw0
+  const float* arow[AI];
+  int aih[AI], aiw[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int row = wid * (BM / NW) + RPI * j + lr;
+    const int lc = pc ^ ((row / RPB) & (CPR - 1));
+    const int m = m0 + row;
+    if (m < M) {
+      const int img = m / HoWo;
+      const int rem = m - img * HoWo;
+      const int oh = rem / a.Wo;
+      const int ow = rem - oh * a.Wo;
+      aih[j] = oh * a.stride - a.pad;
+      aiw[j] = ow * a.stride - a.pad;
+      // STEM: chunk = tap column kw (4 channels each); else chunk = 4 channels of the tap
+      const long long off = (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin;
+      arow[j] = x + off + (STEM ? (long long)lc * a.Cin : lc * 4);
+      if (STEM) aiw[j] += lc;  // this lane's tap column is kw = lc
+    } else {
+      aih[j] = -(1 << 28);
+      aiw[j] = 0;
+      arow[j] = x;
+    }
+  }
+  const float* brow[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int row = wid * (BN / NW) + RPI * j + lr;
+    const int lc = pc ^ ((row / RPB) & (CPR - 1));
+    const int n = n0 + row;
+    brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 4 : nullptr;
+  }
+
+  auto stage = [&](int k0, int slot) {
+    float* As = smem + slot * STAGE;
+    float* Bs = As + BM * BK;
+    int kh, kw, c0;
+    if constexpr (STEM) {
+      kh = k0 / BK;
+      kw = 0;
+      c0 = 0;
+    } else {
+      const int tap = k0 / a.Cin;
+      c0 = k0 - tap * a.Cin;
+      kh = tap / a.KW;
+      kw = tap - kh * a.KW;
+    }
+    const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int ih = aih[j] + kh, iw = aiw[j] + kw;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const float* src = ok ? arow[j] + toff : zero;
+      float* dst = As + (wid * (BM / NW) + RPI * j) * BK;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const float* src = brow[j] ? brow[j] + k0 : zero;
+      float* dst = Bs + (wid * (BN / NW) + RPI * j) * BK;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int h = lane >> 5;
+  const int r = lane & 31;
+  const int sw = (r / RPB) & (CPR - 1);
+  const int nk = a.K / BK;
+  constexpr int PER = AI + BI;  // DMA instructions per stage per wave
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p);
+  if (NS == 3 && nk > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int slot = 0, wslot = NS - 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool issue = kt + NS - 1 < nk;
+    if (issue && !(a.abl & 1)) stage((kt + NS - 1) * BK, wslot);
+    const float* As = smem + slot * STAGE;
+    const float* Bs = As + BM * BK;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const int pch = ((h * (BK / 8) + g) ^ sw) * 4;
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *(const f32x4*)(As + (wm * (BM / WM) + i * 32 + r) * BK + pch);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *(const f32x4*)(Bs + (wn * (BN / WN) + j * 32 + r) * BK + pch);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    }
+    // the next slot's DMA must have landed (leave the newest stage in flight when NS == 3),
+    // and every wave's reads of this slot must be done before anyone refills it
+    if (NS == 3 && issue)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    slot = slot + 1 == NS ? 0 : slot + 1;
+    wslot = wslot + 1 == NS ? 0 : wslot + 1;
+  }
+
+  float* __restrict__ y = (float*)a.y;
+  const float* __restrict__ res = (const float*)a.res;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + r;
+    if (n >= a.Cout) continue;
+    const float b = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm * (BM / WM) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m < M) {
+          const long long o = (long long)m * a.Cout + n;
+          float v = acc[i][j][q] + b;
+          if (res) v += res[o];
+          if (a.relu) v = fmaxf(v, 0.f);
+          if (a.abl & 2) asm volatile("" ::"v"(v)); else y[o] = v;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS = 2>
+static int launch_dma(const ConvArgs& a, hipStream_t s) {
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s,
+                     a);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+// variant 2: BK 32, 128x128 / 128x64 (2 blocks/CU); variant 5: BK 16 (4 blocks/CU)
+int launch_conv_f32_dma(const ConvArgs& a0, hipStream_t s, int variant) {
+  static const int abl = [] {
+    const char* e = getenv("EOSV_CONV_ABL");  // profiling-only ablations; results are wrong when set
+    return e ? atoi(e) : 0;
+  }();
+  ConvArgs a = a0;
+  a.abl = abl;
+  const bool stem = (a.Cin == 4);
+  if (stem) return launch_dma<128, 64, 32, 2, 2, true>(a, s);
+  if (variant == 6) {  // BK 16, 3-deep ring
+    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false, 3>(a, s);
+    return launch_dma<128, 128, 16, 2, 2, false, 3>(a, s);
+  }
+  if (variant == 7) {  // BK 32, 3-deep ring
+    if (a.Cout <= 64) return launch_dma<128, 64, 32, 2, 2, false, 3>(a, s);
+    return launch_dma<128, 128, 32, 2, 2, false, 3>(a, s);
+  }
+  if (variant == 5) {
+    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
+    return launch_dma<128, 128, 16, 2, 2, false>(a, s);
+  }
+  if (a.Cout <= 64) return launch_dma<128, 64, 32, 2, 2, false>(a, s);
+  return launch_dma<128, 128, 32, 2, 2, false>(a, s);
+}
+
+}  // namespace eosv

@@ -46,6 +46,7 @@ struct eosv_handle {
   bool loaded = false;
   size_t act_elems = 0;  // per-frame max activation elements
   void* pack = nullptr;
+  void* zero = nullptr;  // 256 zeroed bytes: DMA source for out-of-bounds conv taps
   void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> allocs;
   int64_t bytes = 0;
@@ -274,6 +275,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   a.pad = c.pad;
   a.K = c.K;
   a.relu = relu ? 1 : 0;
+  a.zero = h->zero;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);
@@ -353,6 +355,8 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   const size_t elt = desc->dtype == EOSV_BF16 ? 2 : 4;
   const size_t F = (size_t)desc->max_frames;
   if (!rc) rc = dmalloc(h, &h->pack, F * desc->height * desc->width * 4 * elt);
+  if (!rc) rc = dmalloc(h, &h->zero, 256);
+  if (!rc && hipMemset(h->zero, 0, 256) != hipSuccess) rc = (set_error("hipMemset zero"), EOSV_ERR_HIP);
   for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);
   if (rc) {
     eosv_destroy(h);

@@ -35,6 +35,7 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
   a.x = dx; a.w = dw; a.bias = db; a.res = res ? dr : nullptr; a.y = dy;
   a.N = N; a.H = H; a.W = W; a.Cin = Cinp; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KH = K; a.KW = K; a.KWp = KWp; a.stride = stride; a.pad = pad; a.K = Kd; a.relu = relu;
+  void* dz; hipMalloc(&dz, 256); hipMemset(dz, 0, 256); a.zero = dz;
   int rc = launch_conv_f32(a, 0);
   hipDeviceSynchronize();
   std::vector<float> y(r.size());
