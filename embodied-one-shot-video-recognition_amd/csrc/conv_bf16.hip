@@ -1,8 +1,228 @@
-// placeholder until the bf16 MFMA conv lands
+// Implicit-GEMM conv on bf16 MFMA (v_mfma_f32_32x32x16_bf16), NHWC bf16 activations,
+// f32 accumulation, folded BN + ReLU + residual in the epilogue, bf16 out.
+//
+// Same structure as conv_f32_dma.hip: A (im2col rows) and B ([Cout][K] weights) move by
+// global_load_lds_dwordx4 into a 2-deep LDS ring, one barrier per K-step.  BK = 64 bf16
+// = 128-B rows (8 x 16-B chunks), XOR swizzle chunk' = chunk ^ ((row >> 1) & 7) applied
+// on the DMA source address.  One 16-B chunk = the 8 consecutive k a lane feeds one MFMA:
+// in MFMA step s of a K-step, lane half h reads chunk 2s + h (k = 16s + 8h .. +7).
+//
+// Stem (Cin 3): the packer writes NHWC4 bf16 rows shifted right by one pixel with zero
+// borders ([0, px0 .. px_{W-1}, 0], W+2 pixels), so the tap pair (p, p+1) that a 16-B
+// chunk holds is 16-B aligned for the odd p = 2*ow - 3 + 2q of a 7x7/2 p3 stem.  K layout
+// [kh 8][kw 8][c 4] (kh 7 and kw 7 zero weights): two kernel rows per K-step.
+#include <hip/hip_bf16.h>
+
 #include "common.h"
+
 namespace eosv {
-int launch_conv_bf16(const ConvArgs&, hipStream_t) {
-  set_error("conv_bf16: not implemented yet");
-  return EOSV_ERR_UNSUPPORTED;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16;
+
+__device__ __forceinline__ float bf_to_f(u16 v) { return __uint_as_float((unsigned)v << 16); }
+__device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
+
+template <int BM, int BN, int WM, int WN, bool STEM>
+__global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
+  constexpr int BK = 64;  // bf16 elements per row = 128 B
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int AI = BM / (8 * NW);
+  constexpr int BI = BN / (8 * NW);
+  constexpr int STAGE = (BM + BN) * BK;  // bf16 elements per ring slot
+  static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile shape");
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int HoWo = a.Ho * a.Wo;
+  const int M = a.N * HoWo;
+  const int nN = (a.Cout + BN - 1) / BN;
+  const int mt = blockIdx.x / nN;
+  const int nt = blockIdx.x - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const u16* __restrict__ x = (const u16*)a.x;
+  const u16* __restrict__ w = (const u16*)a.w;
+  const u16* zero = (const u16*)a.zero;
+
+  const int lr = lane >> 3;
+  const int pc = lane & 7;
+  const int xrow = STEM ? (a.W + 2) * 4 : a.W * a.Cin;  // elements per input row
+  const u16* arow[AI];
+  int aih[AI], aiw[AI], alc[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int row = wid * (BM / NW) + 8 * j + lr;
+    const int lc = pc ^ ((row >> 1) & 7);
+    alc[j] = lc;
+    const int m = m0 + row;
+    if (m < M) {
+      const int img = m / HoWo;
+      const int rem = m - img * HoWo;
+      const int oh = rem / a.Wo;
+      const int ow = rem - oh * a.Wo;
+      aih[j] = oh * a.stride - a.pad;
+      aiw[j] = ow * a.stride - a.pad;
+      if constexpr (STEM) {
+        // chunk lc: kernel row offset lc>>2 within the K-step, tap pair q = lc&3 -> p = iw0 + 2q
+        aiw[j] += 2 * (lc & 3);
+        arow[j] = x + (long long)img * a.H * xrow + (long long)aih[j] * xrow + (long long)(aiw[j] + 1) * 4;
+      } else {
+        arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 8;
+      }
+    } else {
+      aih[j] = -(1 << 28);
+      aiw[j] = 0;
+      arow[j] = x;
+    }
+  }
+  const u16* brow[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int row = wid * (BN / NW) + 8 * j + lr;
+    const int lc = pc ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 8 : nullptr;
+  }
+
+  auto stage = [&](int k0, int slot) {
+    u16* As = smem + slot * STAGE;
+    u16* Bs = As + BM * BK;
+    if constexpr (STEM) {
+      const int kh0 = k0 >> 5;  // 32 k per kernel row
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const int kh = kh0 + (alc[j] >> 2);
+        const int ih = aih[j] + kh;
+        const int p = aiw[j];
+        const bool ok = kh < a.KH && (unsigned)ih < (unsigned)a.H && p >= -1 && p < a.W;
+        const u16* src = ok ? arow[j] + (long long)kh * xrow : zero;
+        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
+    } else {
+      const int tap = k0 / a.Cin;
+      const int c0 = k0 - tap * a.Cin;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+      const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const int ih = aih[j] + kh, iw = aiw[j] + kw;
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const u16* src = ok ? arow[j] + toff : zero;
+        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const u16* src = brow[j] ? brow[j] + k0 : zero;
+      u16* dst = Bs + (wid * (BN / NW) + 8 * j) * BK;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int h = lane >> 5;
+  const int r = lane & 31;
+  const int sw = (r >> 1) & 7;
+  const int nk = a.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage((kt + 1) * BK, cur ^ 1);
+    const u16* As = smem + cur * STAGE;
+    const u16* Bs = As + BM * BK;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int pch = ((2 * s + h) ^ sw) * 8;
+      bf16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(As + (wm * (BM / WM) + i * 32 + r) * BK + pch);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * 32 + r) * BK + pch);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  u16* __restrict__ y = (u16*)a.y;
+  const u16* __restrict__ res = (const u16*)a.res;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + r;
+    if (n >= a.Cout) continue;
+    const float b = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm * (BM / WM) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m < M) {
+          const long long o = (long long)m * a.Cout + n;
+          float v = acc[i][j][q] + b;
+          if (res) v += bf_to_f(res[o]);
+          if (a.relu) v = fmaxf(v, 0.f);
+          y[o] = f_to_bf(v);
+        }
+      }
+    }
+  }
 }
+
+template <int BM, int BN, int WM, int WN, bool STEM>
+static int launch_bf16(const ConvArgs& a, hipStream_t s) {
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+static int bf16_variant() {
+  static int v = [] {
+    const char* e = getenv("EOSV_BF16_TILE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
+  const bool stem = (a.Cin == 4);
+  if (!a.zero || a.K % 64 != 0 || (!stem && a.Cin % 64 != 0) ||
+      (stem && (a.KWp != 8 || a.K != 256 || a.stride != 2 || a.pad != 3 || a.KW != 7))) {
+    set_error("conv_bf16: unsupported shape (K % 64, Cin % 64, or stem layout)");
+    return EOSV_ERR_UNSUPPORTED;
+  }
+  if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
+  if (bf16_variant() == 2) {  // 256x256 tiles, 8 waves of 128x64
+    if (a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);
+    if (a.Cout <= 128) return launch_bf16<256, 128, 4, 2, false>(a, s);
+    return launch_bf16<256, 256, 2, 4, false>(a, s);
+  }
+  if (a.Cout <= 64) return launch_bf16<128, 64, 2, 2, false>(a, s);
+  return launch_bf16<128, 128, 2, 2, false>(a, s);
+}
+
 }  // namespace eosv

@@ -354,7 +354,8 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   int rc = build_plan(h);
   const size_t elt = desc->dtype == EOSV_BF16 ? 2 : 4;
   const size_t F = (size_t)desc->max_frames;
-  if (!rc) rc = dmalloc(h, &h->pack, F * desc->height * desc->width * 4 * elt);
+  if (!rc) rc = dmalloc(h, &h->pack, F * desc->height * (desc->width + 2) * 4 * elt);
+  if (desc->dtype == EOSV_BF16) h->stem.K = 8 * 8 * 4;  // bf16 stem: 2 kernel rows per 64-deep K-step
   if (!rc) rc = dmalloc(h, &h->zero, 256);
   if (!rc && hipMemset(h->zero, 0, 256) != hipSuccess) rc = (set_error("hipMemset zero"), EOSV_ERR_HIP);
   for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);

@@ -27,21 +27,27 @@ __global__ void pack_nchw_nhwc4_kernel(const float* __restrict__ x, long long np
   y[p] = make_float4(src[0], src[HW], src[2 * HW], 0.f);
 }
 
-__global__ void pack_nchw_nhwc4_bf16_kernel(const float* __restrict__ x, long long npix, int HW,
+// bf16: rows shifted right by one pixel with zero borders, [B][H][W+2][4] (see conv_bf16.hip)
+__global__ void pack_nchw_nhwc4_bf16_kernel(const float* __restrict__ x, long long npix, int W, int HW,
                                             ushort4* __restrict__ y) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
   const long long b = p / HW;
   const long long hw = p - b * HW;
+  const long long row = p / W;  // = b*H + y
+  const int xx = (int)(p - row * W);
   const float* src = x + b * 3 * HW + hw;
-  y[p] = make_ushort4(f2bf(src[0]), f2bf(src[HW]), f2bf(src[2 * HW]), 0);
+  ushort4* dst = y + row * (W + 2);
+  dst[xx + 1] = make_ushort4(f2bf(src[0]), f2bf(src[HW]), f2bf(src[2 * HW]), 0);
+  if (xx == 0) dst[0] = make_ushort4(0, 0, 0, 0);
+  if (xx == W - 1) dst[W + 1] = make_ushort4(0, 0, 0, 0);
 }
 
 int launch_pack_nchw_nhwc4(const float* x, int B, int H, int W, void* y, int bf16, hipStream_t s) {
   const long long npix = (long long)B * H * W;
   const unsigned grid = (unsigned)((npix + 255) / 256);
   if (bf16)
-    hipLaunchKernelGGL(pack_nchw_nhwc4_bf16_kernel, dim3(grid), dim3(256), 0, s, x, npix, H * W,
+    hipLaunchKernelGGL(pack_nchw_nhwc4_bf16_kernel, dim3(grid), dim3(256), 0, s, x, npix, W, H * W,
                        (ushort4*)y);
   else
     hipLaunchKernelGGL(pack_nchw_nhwc4_kernel, dim3(grid), dim3(256), 0, s, x, npix, H * W, (float4*)y);

@@ -131,3 +131,35 @@ def test_golden_c1_r18_episodes(r18):
         assert _rel_err(sup[e], arr["support_feature"][e]) < EMB_RTOL
         assert _rel_err(qry[e], arr["query_feature"][e][0]) < EMB_RTOL
     assert np.array_equal(pred.cpu().numpy(), arr["pred"][:, 0])
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_backbone_bf16_close_to_f32_oracle(name):
+    """bf16 path: same architecture, bf16 operands / f32 accumulation.  Acceptance:
+    per-frame feature cosine similarity >= 0.999 and max abs error <= 3% of max |ref|."""
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    bb = engine.Backbone(name, "bf16", 224, 224, max_frames=16)
+    bb.load_state_dict(sd)
+    x = torch.randn(20, 3, 224, 224, generator=torch.Generator().manual_seed(3))
+    out = bb.forward(x.cuda()).cpu().numpy()
+    ref_model = resnet_ref.build_model(name, sd)
+    with torch.no_grad():
+        ref = ref_model(x)[0].numpy()
+    cos = (out * ref).sum(1) / np.linalg.norm(out, axis=1) / np.linalg.norm(ref, axis=1)
+    assert cos.min() > 0.999, cos.min()
+    assert np.abs(out - ref).max() < 0.03 * np.abs(ref).max()
+    bb.close()
+
+
+def test_bf16_episode_agreement():
+    """bf16 predictions on the C1 reference episodes: agreement with the f32 reference
+    predictions >= 90% (the bf16 acceptance rule; f32 is bit-exact)."""
+    meta, arr = load_fixture("c1_r18_protonet_seed1")
+    bb = engine.Backbone("resnet18", "bf16", 224, 224, max_frames=256)
+    bb.load_state_dict(synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0))
+    b = engine.build_episode_batch(meta["episodes"], T=16)
+    dev = engine.DeviceEpisodes(b, 224, 224)
+    pred, emb, _ = engine.run_episodes(bb, dev, "protonet", True)
+    agree = (pred.cpu().numpy() == arr["pred"][:, 0]).mean()
+    assert agree >= 0.9, agree
+    bb.close()
