@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-baseline-sec", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
+    ap.add_argument("--secondary-dtype", default="bf16",
+                    help="also time the same episodes with this backbone dtype ('' to skip)")
     return ap.parse_args()
 
 
@@ -91,6 +93,51 @@ def cpu_baseline(args, episodes, T):
                       f"synthetic-frame generation excluded; {el:.1f}s"}
 
 
+def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
+    """Warmup + timed region for one backbone dtype; returns (elapsed_s, preds, per-layer profile)."""
+    bb = engine.Backbone(args.arch, dtype, args.res, args.res, max_frames=args.max_frames, device=local)
+    bb.load_state_dict(synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
+    feat = torch.empty(max(d.batch.n_frames for d in batches), bb.D, device=f"cuda:{local}")
+    for s in range(args.warmup):
+        d = batches[s]
+        engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    bb.profile(True)
+    preds = []
+    t0 = time.perf_counter()
+    for s in range(args.warmup, len(batches)):
+        d = batches[s]
+        p, _, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
+        preds.append(p)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof = bb.profile_read()
+    bb.profile(False)
+    bb.close()
+    if dist:
+        el_t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(el_t.item())
+    return elapsed, torch.cat(preds), prof
+
+
+def roofline(prof, dtype, launches_label=True):
+    ms, fl, nl = prof
+    conv_ms, conv_fl = float(ms.sum()), float(fl.sum())
+    achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    peak = MFMA_PEAK_TF[dtype]
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
+                      f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -108,48 +155,19 @@ def main():
     n_steps = args.warmup + args.steps
     plans = ep_mod.sample_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed)
     mine = ep_mod.shard(plans, rank, world)
-    bb = engine.Backbone(args.arch, args.dtype, args.res, args.res, max_frames=args.max_frames,
-                         device=local)
-    bb.load_state_dict(synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
     batches = []
     for s in range(n_steps):
         b = engine.build_episode_batch(mine[s * E:(s + 1) * E], T)
         batches.append(engine.DeviceEpisodes(b, args.res, args.res, device=local))
-    feat = torch.empty(max(d.batch.n_frames for d in batches), bb.D, device=f"cuda:{local}")
     torch.cuda.synchronize()
 
-    preds = []
-    for s in range(args.warmup):
-        d = batches[s]
-        p, _, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    bb.profile(True)
-    t0 = time.perf_counter()
-    for s in range(args.warmup, n_steps):
-        d = batches[s]
-        p, _, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
-        preds.append(p)
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ms, fl, nl = bb.profile_read()
-    bb.profile(False)
-
+    elapsed, pred, prof = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
     clips = sum(d.batch.n_clips for d in batches[args.warmup:])
     frames = sum(d.batch.n_frames for d in batches[args.warmup:])
-    # results: (pred, correct) per episode, all-gathered over xGMI
-    pred = torch.cat(preds)
+    # results: (pred, correct) per episode, all-gathered once over xGMI (RCCL)
     qy = torch.from_numpy(np.concatenate([d.batch.query_y for d in batches[args.warmup:]])).to(pred.device)
     res = torch.stack([pred.to(torch.int32), (pred == qy).to(torch.int32)], 1)
     if dist:
-        el_t = torch.tensor([elapsed], device=pred.device, dtype=torch.float64)
-        tdist.all_reduce(el_t, op=tdist.ReduceOp.MAX)
-        elapsed = float(el_t.item())
         tot = torch.tensor([clips, frames], device=pred.device, dtype=torch.int64)
         tdist.all_reduce(tot)
         clips, frames = int(tot[0]), int(tot[1])
@@ -158,14 +176,26 @@ def main():
         res = torch.cat(gathered)
     acc = float(res[:, 1].float().mean().item())
 
+    secondary = None
+    if args.secondary_dtype and args.secondary_dtype != args.dtype:
+        el2, pred2, prof2 = run_timed(args, engine, arch_mod, synth, batches, args.secondary_dtype, local, dist)
+        agree = (pred2 == pred).float().mean()
+        if dist:
+            tdist.all_reduce(agree)
+            agree = agree / world
+        secondary = {"dtype": args.secondary_dtype, "value": round(clips / el2, 2), "unit": "clips/s",
+                     "ms_per_step": round(el2 / args.steps * 1e3, 3),
+                     "prediction_agreement_vs_primary": round(float(agree), 4),
+                     "roofline": roofline(prof2, args.secondary_dtype)}
+
     if rank == 0:
-        conv_ms, conv_fl = float(ms.sum()), float(fl.sum())
-        launches = int(nl.sum())
-        achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-        peak = MFMA_PEAK_TF[args.dtype]
+        ms, fl, nl = prof
         gflop_frame = 2 * arch_mod.conv_macs_per_frame(arch_mod.SPECS[args.arch], args.res, args.res) / 1e9
+        rl = roofline(prof, args.dtype)
+        rl["end_to_end_tflops"] = round(frames * gflop_frame / elapsed / 1e3, 2)
+        rl["flop_per_frame"] = round(gflop_frame * 1e9)
         out = {
-            "metric": "clips/sec/GPU (224², 8-seg) + 5-way-1-shot episode acc vs reference",
+            "metric": "clips/sec/GPU (224\u00b2, 8-seg) + 5-way-1-shot episode acc vs reference",
             "value": round(clips / elapsed, 2),
             "unit": "clips/s",
             "n_gpus": world,
@@ -185,14 +215,11 @@ def main():
                        "frames_per_clip": T, "parallelism": f"episode-sharded dp{world}"},
             "frames_per_s": round(frames / elapsed, 1),
             "episode_acc": round(acc, 4),
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
-                         "kernel": f"conv_{args.dtype}_kernel (all {launches} conv launches of the timed "
-                                   f"region, HIP events on the launch stream)",
-                         "flop_per_frame": round(gflop_frame * 1e9),
-                         "end_to_end_tflops": round(frames * gflop_frame / elapsed / 1e3, 2)},
+            "roofline": rl,
             "cpu_baseline": None,
         }
+        if secondary:
+            out["secondary"] = secondary
         if args.layers:
             for i in range(len(ms)):
                 if nl[i]:

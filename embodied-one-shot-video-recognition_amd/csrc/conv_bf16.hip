@@ -203,7 +203,7 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
 static int bf16_variant() {
   static int v = [] {
     const char* e = getenv("EOSV_BF16_TILE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 3;
   }();
   return v;
 }
@@ -216,6 +216,7 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
+  if (bf16_variant() == 3 && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
   if (bf16_variant() == 2) {  // 256x256 tiles, 8 waves of 128x64
     if (a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);
     if (a.Cout <= 128) return launch_bf16<256, 128, 4, 2, false>(a, s);
