@@ -120,11 +120,8 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     prof = bb.profile_read()
     bb.profile(False)
     bb.close()
-    if dist:
-        el_t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
-        torch.distributed.all_reduce(el_t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(el_t.item())
-    return elapsed, torch.cat(preds), prof
+    from eosv import dist as edist
+    return edist.max_over_ranks(elapsed), torch.cat(preds), prof
 
 
 def roofline(prof, dtype, launches_label=True):
@@ -147,45 +144,39 @@ def main():
     torch.cuda.set_device(local)
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from eosv import arch as arch_mod, engine, episodes as ep_mod, synth  # noqa
+        backend = os.environ.get("EOSV_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        tdist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
+    from eosv import arch as arch_mod, dist as edist, engine, episodes as ep_mod, synth  # noqa
 
     T = args.segments * args.seg_len
     E = args.episodes_per_step
     n_steps = args.warmup + args.steps
     plans = ep_mod.sample_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed)
-    mine = ep_mod.shard(plans, rank, world)
+    mine_idx = edist.shard_indices(len(plans), rank, world)  # episode e runs on rank e % world
     batches = []
     for s in range(n_steps):
-        b = engine.build_episode_batch(mine[s * E:(s + 1) * E], T)
+        b = engine.build_episode_batch([plans[e] for e in mine_idx[s * E:(s + 1) * E]], T)
         batches.append(engine.DeviceEpisodes(b, args.res, args.res, device=local))
     torch.cuda.synchronize()
+    timed_idx = mine_idx[args.warmup * E:]
 
     elapsed, pred, prof = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
-    clips = sum(d.batch.n_clips for d in batches[args.warmup:])
-    frames = sum(d.batch.n_frames for d in batches[args.warmup:])
-    # results: (pred, correct) per episode, all-gathered once over xGMI (RCCL)
-    qy = torch.from_numpy(np.concatenate([d.batch.query_y for d in batches[args.warmup:]])).to(pred.device)
-    res = torch.stack([pred.to(torch.int32), (pred == qy).to(torch.int32)], 1)
-    if dist:
-        tot = torch.tensor([clips, frames], device=pred.device, dtype=torch.int64)
-        tdist.all_reduce(tot)
-        clips, frames = int(tot[0]), int(tot[1])
-        gathered = [torch.empty_like(res) for _ in range(world)]
-        tdist.all_gather(gathered, res)
-        res = torch.cat(gathered)
-    acc = float(res[:, 1].float().mean().item())
+    clips = edist.sum_over_ranks(sum(d.batch.n_clips for d in batches[args.warmup:]))
+    frames = edist.sum_over_ranks(sum(d.batch.n_frames for d in batches[args.warmup:]))
+    # (episode, prediction) pairs: ONE all-gather over xGMI (RCCL) after the timed region
+    preds = edist.gather_predictions(timed_idx, pred.cpu().numpy(), len(plans))
+    timed = preds >= 0
+    qy = np.array([p["query_y"] for p in plans])
+    acc = float((preds[timed] == qy[timed]).mean())
 
     secondary = None
     if args.secondary_dtype and args.secondary_dtype != args.dtype:
         el2, pred2, prof2 = run_timed(args, engine, arch_mod, synth, batches, args.secondary_dtype, local, dist)
-        agree = (pred2 == pred).float().mean()
-        if dist:
-            tdist.all_reduce(agree)
-            agree = agree / world
+        preds2 = edist.gather_predictions(timed_idx, pred2.cpu().numpy(), len(plans))
         secondary = {"dtype": args.secondary_dtype, "value": round(clips / el2, 2), "unit": "clips/s",
                      "ms_per_step": round(el2 / args.steps * 1e3, 3),
-                     "prediction_agreement_vs_primary": round(float(agree), 4),
+                     "prediction_agreement_vs_primary": round(float((preds2[timed] == preds[timed]).mean()), 4),
+                     "episode_acc": round(float((preds2[timed] == qy[timed]).mean()), 4),
                      "roofline": roofline(prof2, args.secondary_dtype)}
 
     if rank == 0:
@@ -226,7 +217,7 @@ def main():
                     print(f"layer {i:3d}: {ms[i] / nl[i]:8.3f} ms/launch  {fl[i] / ms[i] / 1e9:7.2f} TF/s",
                           file=sys.stderr)
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, mine[:50], T)
+            out["cpu_baseline"] = cpu_baseline(args, [plans[e] for e in mine_idx[:50]], T)
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

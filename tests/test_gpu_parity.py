@@ -163,3 +163,17 @@ def test_bf16_episode_agreement():
     agree = (pred.cpu().numpy() == arr["pred"][:, 0]).mean()
     assert agree >= 0.9, agree
     bb.close()
+
+
+@pytest.mark.parametrize("name,res", [("resnet50", 224), ("resnet101", 256), ("resnet18", 112)])
+def test_backbone_f32_other_archs(name, res):
+    """R50 / R101 (config 5's backbone, 256x256) / small frames: f32 path vs the oracle."""
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    bb = engine.Backbone(name, "f32", res, res, max_frames=3)  # B > max_frames exercises chunking
+    bb.load_state_dict(sd)
+    x = torch.randn(5, 3, res, res, generator=torch.Generator().manual_seed(11))
+    out = bb.forward(x.cuda()).cpu().numpy()
+    with torch.no_grad():
+        ref = resnet_ref.build_model(name, sd)(x)[0].numpy()
+    assert _rel_err(out, ref) < 2e-5
+    bb.close()
