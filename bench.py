@@ -170,7 +170,7 @@ def main():
     acc = float((preds[timed] == qy[timed]).mean())
 
     secondary = None
-    if args.secondary_dtype and args.secondary_dtype != args.dtype:
+    if args.secondary_dtype and args.secondary_dtype not in ("none", args.dtype):
         el2, pred2, prof2 = run_timed(args, engine, arch_mod, synth, batches, args.secondary_dtype, local, dist)
         preds2 = edist.gather_predictions(timed_idx, pred2.cpu().numpy(), len(plans))
         secondary = {"dtype": args.secondary_dtype, "value": round(clips / el2, 2), "unit": "clips/s",

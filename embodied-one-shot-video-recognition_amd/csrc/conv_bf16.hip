@@ -168,24 +168,61 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 
   u16* __restrict__ y = (u16*)a.y;
   const u16* __restrict__ res = (const u16*)a.res;
+  // Epilogue staged through LDS (the ring is free now): pass i moves the i-th 32-row
+  // M-subtile of every wave (WM*32 rows x BN cols, f32, rows padded by 4) so that the
+  // residual loads and output stores are 16 B (8 bf16) per lane, whole 128-B lines.
+  constexpr int EPR = WM * 32;   // rows per pass
+  constexpr int EPS = BN + 4;    // f32 row stride
+  static_assert(EPR * EPS * 4 <= 2 * STAGE * 2, "epilogue tile must fit the ring");
+  float* ep = (float*)smem;
+  float bcol[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 32 + r;
-    if (n >= a.Cout) continue;
-    const float b = a.bias ? a.bias[n] : 0.f;
+    bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+  }
+  const int nthreads = 64 * NW;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+  for (int i = 0; i < TM; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int m = m0 + wm * (BM / WM) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (m < M) {
-          const long long o = (long long)m * a.Cout + n;
-          float v = acc[i][j][q] + b;
-          if (res) v += bf_to_f(res[o]);
-          if (a.relu) v = fmaxf(v, 0.f);
-          y[o] = f_to_bf(v);
+        const int lrow = wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        ep[lrow * EPS + wn * (BN / WN) + j * 32 + r] = acc[i][j][q] + bcol[j];
+      }
+    __syncthreads();
+    for (int idx = tid; idx < EPR * (BN / 8); idx += nthreads) {
+      const int lrow = idx / (BN / 8);
+      const int c8 = idx - lrow * (BN / 8);
+      const int m = m0 + (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
+      const int n = n0 + c8 * 8;
+      if (m >= M || n >= a.Cout) continue;
+      const float4 v0 = *(const float4*)(ep + lrow * EPS + c8 * 8);
+      const float4 v1 = *(const float4*)(ep + lrow * EPS + c8 * 8 + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      const long long o = (long long)m * a.Cout + n;
+      if (res) {
+        const uint4 rv = *(const uint4*)(res + o);
+        const unsigned ru[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff));
+          v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16));
         }
       }
+      unsigned pk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float lo = v[2 * k], hi = v[2 * k + 1];
+        if (a.relu) {
+          lo = fmaxf(lo, 0.f);
+          hi = fmaxf(hi, 0.f);
+        }
+        pk[k] = (unsigned)f_to_bf(lo) | ((unsigned)f_to_bf(hi) << 16);
+      }
+      *(uint4*)(y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     }
   }
 }

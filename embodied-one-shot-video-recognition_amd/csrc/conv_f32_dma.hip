@@ -21,7 +21,7 @@ namespace eosv {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS>
+template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS, bool EPI_LDS>
 __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 32;
@@ -174,11 +174,66 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
 
   float* __restrict__ y = (float*)a.y;
   const float* __restrict__ res = (const float*)a.res;
+  float bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + r;
+    bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+  }
+  if constexpr (EPI_LDS) {
+    // Epilogue staged through LDS (the ring is free): pass (i, wsel) moves the 32 x BN rows
+    // of M-subtile i of the waves with wm == wsel, so residual loads / output stores are
+    // 16 B per lane over whole 128-B lines.
+    constexpr int EPS = BN + 4;
+    static_assert(32 * EPS <= NS * STAGE, "epilogue slab must fit the ring");
+    float* ep = smem;
+    const int nthreads = 64 * NW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      for (int wsel = 0; wsel < WM; ++wsel) {
+        __syncthreads();
+        if (wm == wsel) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+              ep[((q & 3) + 8 * (q >> 2) + 4 * h) * EPS + wn * (BN / WN) + j * 32 + r] = acc[i][j][q] + bcol[j];
+        }
+        __syncthreads();
+        for (int idx = tid; idx < 32 * (BN / 4); idx += nthreads) {
+          const int lrow = idx / (BN / 4);
+          const int c4 = idx - lrow * (BN / 4);
+          const int m = m0 + wsel * (BM / WM) + i * 32 + lrow;
+          const int n = n0 + c4 * 4;
+          if (m >= M || n >= a.Cout) continue;
+          float4 v = *(const float4*)(ep + lrow * EPS + c4 * 4);
+          const long long o = (long long)m * a.Cout + n;
+          if (res) {
+            const float4 rv = *(const float4*)(res + o);
+            v.x += rv.x;
+            v.y += rv.y;
+            v.z += rv.z;
+            v.w += rv.w;
+          }
+          if (a.relu) {
+            v.x = fmaxf(v.x, 0.f);
+            v.y = fmaxf(v.y, 0.f);
+            v.z = fmaxf(v.z, 0.f);
+            v.w = fmaxf(v.w, 0.f);
+          }
+          if (a.abl & 2)
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+          else
+            *(float4*)(y + o) = v;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 32 + r;
     if (n >= a.Cout) continue;
-    const float b = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -186,7 +241,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
         const int m = m0 + wm * (BM / WM) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
         if (m < M) {
           const long long o = (long long)m * a.Cout + n;
-          float v = acc[i][j][q] + b;
+          float v = acc[i][j][q] + bcol[j];
           if (res) v += res[o];
           if (a.relu) v = fmaxf(v, 0.f);
           if (a.abl & 2) asm volatile("" ::"v"(v)); else y[o] = v;
@@ -196,12 +251,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS = 2>
+template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS = 2, bool EPI = true>
 static int launch_dma(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s,
+  hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS, EPI>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s,
                      a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
@@ -217,9 +272,9 @@ int launch_conv_f32_dma(const ConvArgs& a0, hipStream_t s, int variant) {
   a.abl = abl;
   const bool stem = (a.Cin == 4);
   if (stem) return launch_dma<128, 64, 32, 2, 2, true>(a, s);
-  if (variant == 6) {  // BK 16, 3-deep ring
-    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false, 3>(a, s);
-    return launch_dma<128, 128, 16, 2, 2, false, 3>(a, s);
+  if (variant == 6) {  // BK 16, 2-deep ring, per-lane epilogue stores (pre-LDS-epilogue baseline)
+    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);
+    return launch_dma<128, 128, 16, 2, 2, false, 2, false>(a, s);
   }
   if (variant == 7) {  // BK 32, 3-deep ring
     if (a.Cout <= 64) return launch_dma<128, 64, 32, 2, 2, false, 3>(a, s);
