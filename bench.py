@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--k-shot", type=int, default=1)
     ap.add_argument("--segments", type=int, default=8)
     ap.add_argument("--seg-len", type=int, default=2)
-    ap.add_argument("--max-frames", type=int, default=1024)
+    ap.add_argument("--max-frames", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-baseline-sec", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

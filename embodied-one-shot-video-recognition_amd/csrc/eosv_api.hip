@@ -407,8 +407,12 @@ int eosv_backbone_forward(eosv_handle* h, const float* d_frames, int B, float* d
     return EOSV_ERR_STATE;
   }
   const size_t fstride = (size_t)3 * h->d.height * h->d.width;
-  for (int b0 = 0; b0 < B; b0 += h->d.max_frames) {
-    const int nb = std::min(h->d.max_frames, B - b0);
+  // equal-size chunks (no small tail chunk): fewer, fuller launches
+  const int nchunks = (B + h->d.max_frames - 1) / h->d.max_frames;
+  const int csz = nchunks ? (B + nchunks - 1) / nchunks : 0;
+  for (int b0 = 0; b0 < B; b0 += csz) {
+    const int nb = std::min(csz, B - b0);
+
     int rc = forward_chunk(h, d_frames + b0 * fstride, nb, d_feat + (size_t)b0 * h->D,
                            (hipStream_t)stream);
     if (rc) return rc;
