@@ -48,6 +48,11 @@ struct eosv_handle {
   void* pack = nullptr;
   void* zero = nullptr;  // 256 zeroed bytes: DMA source for out-of-bounds conv taps
   void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* sbuf[4] = {nullptr, nullptr, nullptr, nullptr};  // sub-chunk scratch for the front stages
+  int sub_frames = 0;          // front-stage sub-chunk (0 = off)
+  size_t n_front = 0;          // blocks in the front phase (layer1)
+  size_t front_out_elems = 0;  // per-frame elements of the layer1 output
+  int front_hw[2] = {0, 0};
   std::vector<void*> allocs;
   int64_t bytes = 0;
   int n_layers = 0;
@@ -145,6 +150,12 @@ static int build_plan(eosv_handle* h) {
       hh = ho;
       ww = wo;
       inpl = cout;
+      if (li == 0) {
+        h->n_front = h->blocks.size();
+        h->front_out_elems = (size_t)hh * ww * cout;
+        h->front_hw[0] = hh;
+        h->front_hw[1] = ww;
+      }
     }
   }
   h->act_elems = act;
@@ -292,21 +303,18 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   return rc;
 }
 
-static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat, hipStream_t s) {
-  const bool bf = h->d.dtype == EOSV_BF16;
-  const int H = h->d.height, W = h->d.width;
+// Residual blocks [b0, b1) on x (B frames, hh x ww) using the 4-buffer set `bufs`.  The
+// output of each block lands in place of its residual buffer; when `dst` is given, the last
+// block writes there instead (its residual still comes from `bufs`).
+static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const* bufs, int B, int& hh,
+                      int& ww, void* dst, void** xout, bool bf, hipStream_t s) {
   int rc;
-  if ((rc = launch_pack_nchw_nhwc4(frames, B, H, W, h->pack, bf, s))) return rc;
-  if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, h->buf[0], true, bf, s))) return rc;
-  if ((rc = launch_maxpool3x3s2(h->buf[0], B, h->hs, h->ws, 64, h->buf[1], h->hp, h->wp, bf, s)))
-    return rc;
-  void* x = h->buf[1];
-  int hh = h->hp, ww = h->wp;
-  for (const Block& b : h->blocks) {
+  for (size_t bi = b0; bi < b1; ++bi) {
+    const Block& b = h->blocks[bi];
     void* fr[3];
     int nf = 0;
-    for (void* p : h->buf)
-      if (p != x) fr[nf++] = p;
+    for (int k = 0; k < 4; ++k)
+      if (bufs[k] != x) fr[nf++] = bufs[k];
     const int st = b.bottleneck ? b.c2.stride : b.c1.stride;  // torchvision: stride on the 3x3
     const int ho = conv_out(hh, 3, st, 1), wo = conv_out(ww, 3, st, 1);
     void* r = x;
@@ -314,18 +322,58 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
       r = fr[2];
       if ((rc = run_conv(h, b.ds, x, B, hh, ww, nullptr, r, false, bf, s))) return rc;
     }
+    void* y = (dst && bi + 1 == b1) ? dst : r;
     if (!b.bottleneck) {
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
-      if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, r, r, true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, r, y, true, bf, s))) return rc;
     } else {
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
       if ((rc = run_conv(h, b.c2, fr[0], B, hh, ww, nullptr, fr[1], true, bf, s))) return rc;
-      if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, r, r, true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, r, y, true, bf, s))) return rc;
     }
-    x = r;
+    x = y;
     hh = ho;
     ww = wo;
   }
+  *xout = x;
+  return EOSV_OK;
+}
+
+// stem -> maxpool -> stage-0 blocks for frames [0, B) of `frames`, output into `dst`
+static int run_front(eosv_handle* h, const float* frames, int B, void* const* bufs, void* dst, void** xout,
+                     bool bf, hipStream_t s) {
+  const int H = h->d.height, W = h->d.width;
+  int rc;
+  if ((rc = launch_pack_nchw_nhwc4(frames, B, H, W, h->pack, bf, s))) return rc;
+  if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, bufs[0], true, bf, s))) return rc;
+  if ((rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s))) return rc;
+  int hh = h->hp, ww = h->wp;
+  return run_blocks(h, 0, h->n_front, bufs[1], bufs, B, hh, ww, dst, xout, bf, s);
+}
+
+static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat, hipStream_t s) {
+  const bool bf = h->d.dtype == EOSV_BF16;
+  const size_t elt = bf ? 2 : 4;
+  int rc;
+  void* x;
+  int hh = h->hp, ww = h->wp;
+  if (h->sub_frames > 0 && h->sub_frames < B) {
+    // Front stages (stem, maxpool, layer1: the largest activations) run on sub-chunks whose
+    // working set stays in the 256 MiB Infinity Cache; each sub-chunk's layer1 output lands
+    // in the full-size buffer buf[1], from which layer2..4 run on the whole chunk.
+    const size_t fstride = (size_t)3 * h->d.height * h->d.width;
+    for (int s0 = 0; s0 < B; s0 += h->sub_frames) {
+      const int nb = std::min(h->sub_frames, B - s0);
+      void* dst = (char*)h->buf[1] + (size_t)s0 * h->front_out_elems * elt;
+      if ((rc = run_front(h, frames + s0 * fstride, nb, h->sbuf, dst, &x, bf, s))) return rc;
+    }
+    x = h->buf[1];
+  } else {
+    if ((rc = run_front(h, frames, B, h->buf, nullptr, &x, bf, s))) return rc;
+  }
+  hh = h->front_hw[0];
+  ww = h->front_hw[1];
+  if ((rc = run_blocks(h, h->n_front, h->blocks.size(), x, h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
   return launch_avgpool(x, B, hh * ww, h->D, feat, bf, s);
 }
 
@@ -359,6 +407,15 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   if (!rc) rc = dmalloc(h, &h->zero, 256);
   if (!rc && hipMemset(h->zero, 0, 256) != hipSuccess) rc = (set_error("hipMemset zero"), EOSV_ERR_HIP);
   for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);
+  {
+    // front-stage sub-chunk: keeps stem/layer1 activations Infinity-Cache resident
+    const char* e = getenv("EOSV_SUB_FRAMES");
+    int sub = e ? atoi(e) : 0;  // measured: no gain at 64..256 (R18 f32/bf16, R50 bf16)
+    if (sub > 0 && sub < desc->max_frames) {
+      h->sub_frames = sub;
+      for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->sbuf[i], (size_t)sub * h->act_elems * elt);
+    }
+  }
   if (rc) {
     eosv_destroy(h);
     return rc;
