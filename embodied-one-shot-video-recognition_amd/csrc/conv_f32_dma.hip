@@ -280,6 +280,15 @@ int launch_conv_f32_dma(const ConvArgs& a0, hipStream_t s, int variant) {
     if (a.Cout <= 64) return launch_dma<128, 64, 32, 2, 2, false, 3>(a, s);
     return launch_dma<128, 128, 32, 2, 2, false, 3>(a, s);
   }
+  if (variant == 9) {  // BK 16, 256-row tiles (8 waves for Cout >= 128)
+    if (a.Cout <= 64) return launch_dma<256, 64, 16, 4, 1, false>(a, s);
+    return launch_dma<256, 128, 16, 4, 2, false>(a, s);
+  }
+  if (variant == 10) {  // BK 16, 128x256 for Cout >= 256 (wave 64x128)
+    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
+    if (a.Cout <= 128) return launch_dma<128, 128, 16, 2, 2, false>(a, s);
+    return launch_dma<128, 256, 16, 2, 2, false>(a, s);
+  }
   if (variant == 5) {
     if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
     return launch_dma<128, 128, 16, 2, 2, false>(a, s);
