@@ -112,6 +112,13 @@ int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G,
 int eosv_temporal_smooth(const float* d_x, int rows, int cols, float lamda1, float lamda2,
                          float* d_y, eosv_stream_t stream);
 
+/* Frame ingest (utils.py:80-91 test transform): d_rgb [n_frames, H, W, 3] uint8 decoded
+ * frames -> centre crop `crop` -> /255 -> (x - mean[c]) / std[c] -> d_out [n_frames,3,crop,crop]
+ * f32 NCHW.  mean/std are HOST arrays of 3 floats.  Bit-identical to torchvision's
+ * CenterCrop + ToTensor + Normalize on the same pixels. */
+int eosv_normalize_frames(const uint8_t* d_rgb, int n_frames, int H, int W, int crop, const float* mean,
+                          const float* std, float* d_out, eosv_stream_t stream);
+
 /* Deterministic synthetic frames, bit-identical to eosv/synth.py:synth_frame.
  * For frame f: class seed, video seed, noise seed (u64) and frame id in d_params
  * [n_frames, 4] (u64); writes d_frames [n_frames,3,H,W] f32 NCHW.  Frames with

@@ -177,3 +177,15 @@ def test_backbone_f32_other_archs(name, res):
         ref = resnet_ref.build_model(name, sd)(x)[0].numpy()
     assert _rel_err(out, ref) < 2e-5
     bb.close()
+
+
+def test_normalize_frames_bit_exact_vs_host_transform():
+    """Fused ingest kernel == the host restatement of CenterCrop/ToTensor/Normalize."""
+    from eosv import frames as fr
+    rng = np.random.default_rng(4)
+    rgb = rng.integers(0, 256, size=(3, 256, 341, 3), dtype=np.uint8)
+    out = engine.normalize_frames(torch.from_numpy(rgb).cuda(), 224).cpu().numpy()
+    top, left = int(round((256 - 224) / 2.0)), int(round((341 - 224) / 2.0))
+    a = rgb[:, top:top + 224, left:left + 224].astype(np.float32) / np.float32(255.0)
+    ref = ((a - fr.MEAN) / fr.STD).transpose(0, 3, 1, 2)
+    assert np.array_equal(out.view(np.uint32), np.ascontiguousarray(ref).view(np.uint32))
