@@ -190,7 +190,7 @@ static int launch_v1(const ConvArgs& a, hipStream_t s) {
 static int conv_impl() {
   static int v = [] {
     const char* e = getenv("EOSV_CONV_IMPL");
-    return e ? atoi(e) : 5;
+    return e ? atoi(e) : 11;
   }();
   return v;
 }
