@@ -32,8 +32,8 @@ void set_error(const std::string& msg);
 
 // ------------------------------------------------------------------ conv
 struct ConvArgs {
-  const void* x;      // NHWC input [N,H,W,Cin]  (stem: Cin = 4, channel 3 zero)
-  const void* w;      // [Cout][K]: K ordered (kh, kw_padded, cin)
+  const void* x;      // NHWC input [N,H,W,Cin]  (stem, Cin = 3: padded [N][H+2p][Wp][3])
+  const void* w;      // [Cout][K]: K ordered (kh, kw_padded, cin); stem (kh, kw*3 + c) 24 per kh
   const float* bias;  // [Cout] folded BN shift
   const void* res;    // NHWC residual [N,Ho,Wo,Cout] or nullptr
   void* y;            // NHWC output [N,Ho,Wo,Cout]
@@ -51,8 +51,13 @@ int launch_conv_f32_dma(const ConvArgs& a, hipStream_t s, int variant);
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ layout / pooling
-int launch_pack_nchw_nhwc4(const float* x, int B, int H, int W, void* y, int bf16,
-                           hipStream_t s);
+// stem input layout: zero-bordered RGB rows of stem_row_pixels(W, pad) pixels (even, so the
+// stem's bf16 DMA sources stay 4-B aligned)
+inline int stem_row_pixels(int W, int pad) { return (W + 2 * pad + 1) & ~1; }
+inline size_t stem_input_elems(int B, int H, int W, int pad) {
+  return (size_t)B * (H + 2 * pad) * stem_row_pixels(W, pad) * 3 + 64;  // + over-read slack
+}
+int launch_pack_rgb_pad(const float* x, int B, int H, int W, int pad, void* y, int bf16, hipStream_t s);
 int launch_maxpool3x3s2(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo,
                         int bf16, hipStream_t s);
 int launch_avgpool(const void* x, int B, int HW, int C, float* y, int bf16, hipStream_t s);

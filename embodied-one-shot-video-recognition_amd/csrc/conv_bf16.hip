@@ -7,10 +7,13 @@
 // on the DMA source address.  One 16-B chunk = the 8 consecutive k a lane feeds one MFMA:
 // in MFMA step s of a K-step, lane half h reads chunk 2s + h (k = 16s + 8h .. +7).
 //
-// Stem (Cin 3): the packer writes NHWC4 bf16 rows shifted right by one pixel with zero
-// borders ([0, px0 .. px_{W-1}, 0], W+2 pixels), so the tap pair (p, p+1) that a 16-B
-// chunk holds is 16-B aligned for the odd p = 2*ow - 3 + 2q of a 7x7/2 p3 stem.  K layout
-// [kh 8][kw 8][c 4] (kh 7 and kw 7 zero weights): two kernel rows per K-step.
+// Stem (Cin 3): dense padded RGB input [N][H+2p][Wp][3] bf16 (Wp = W+2p rounded up to even)
+// with zero borders; K laid
+// out [kh][24] (kw*3 + c: 21 real + 3 zero weights) = 21 16-B chunks, padded to 192 = 3
+// K-steps (77 % of the MFMA work real; NHWC4 with kw padded to 8 and K 256: 57 %).  Chunk
+// g = 8*kt + lc is kernel row g / 3, elements 8*(g % 3) .. +7 of that row's tap run; the
+// 16-B DMA source is only 4-B aligned there (even padded row width, even stride; LDS-DMA
+// accepts that: tests/native/dma_probe.cpp).
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -52,7 +55,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 
   const int lr = lane >> 3;
   const int pc = lane & 7;
-  const int xrow = STEM ? (a.W + 2) * 4 : a.W * a.Cin;  // elements per input row
+  const int xrow = ((a.W + 2 * a.pad + 1) & ~1) * 3;  // STEM: elements per padded input row
   const u16* arow[AI];
   int aih[AI], aiw[AI], alc[AI];
 #pragma unroll
@@ -69,9 +72,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
       aih[j] = oh * a.stride - a.pad;
       aiw[j] = ow * a.stride - a.pad;
       if constexpr (STEM) {
-        // chunk lc: kernel row offset lc>>2 within the K-step, tap pair q = lc&3 -> p = iw0 + 2q
-        aiw[j] += 2 * (lc & 3);
-        arow[j] = x + (long long)img * a.H * xrow + (long long)aih[j] * xrow + (long long)(aiw[j] + 1) * 4;
+        // padded coordinates of tap (0, 0) are (oh*stride, ow*stride)
+        arow[j] = x + ((long long)img * (a.H + 2 * a.pad) + oh * a.stride) * xrow + (long long)ow * a.stride * 3;
       } else {
         arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 8;
       }
@@ -94,14 +96,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     u16* As = smem + slot * STAGE;
     u16* Bs = As + BM * BK;
     if constexpr (STEM) {
-      const int kh0 = k0 >> 5;  // 32 k per kernel row
 #pragma unroll
       for (int j = 0; j < AI; ++j) {
-        const int kh = kh0 + (alc[j] >> 2);
-        const int ih = aih[j] + kh;
-        const int p = aiw[j];
-        const bool ok = kh < a.KH && (unsigned)ih < (unsigned)a.H && p >= -1 && p < a.W;
-        const u16* src = ok ? arow[j] + (long long)kh * xrow : zero;
+        const int g = (k0 >> 3) + alc[j];
+        const int kh = g / 3;
+        const bool ok = aih[j] > -(1 << 27) && kh < a.KH;
+        const u16* src = ok ? arow[j] + kh * xrow + (g - 3 * kh) * 8 : zero;
         u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
@@ -246,9 +246,9 @@ static int bf16_variant() {
 }
 
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
-  const bool stem = (a.Cin == 4);
+  const bool stem = (a.Cin == 3);
   if (!a.zero || a.K % 64 != 0 || (!stem && a.Cin % 64 != 0) ||
-      (stem && (a.KWp != 8 || a.K != 256 || a.stride != 2 || a.pad != 3 || a.KW != 7))) {
+      (stem && (a.KWp != 8 || a.KW != 7 || a.stride % 2 != 0 || a.K != (a.KH * 24 + 63) / 64 * 64))) {
     set_error("conv_bf16: unsupported shape (K % 64, Cin % 64, or stem layout)");
     return EOSV_ERR_UNSUPPORTED;
   }

@@ -22,7 +22,7 @@ namespace eosv {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int BM, int BN, bool STEM>
+template <int BM, int BN>
 __global__ __launch_bounds__(256) void conv_f32_kernel(ConvArgs a) {
   constexpr int BK = 32;
   constexpr int LDK = BK + 4;
@@ -72,23 +72,15 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(ConvArgs a) {
 
   f32x4 ra[AR], rb[BR];
   auto load = [&](int k0) {
-    int kh, kw, c0;
-    if constexpr (STEM) {
-      kh = k0 >> 5;  // one kernel row (8 padded taps x 4 channels) per BK chunk
-      kw = kq;
-      c0 = 0;
-    } else {
-      const int tap = k0 / a.Cin;
-      c0 = k0 - tap * a.Cin + kq * 4;
-      kh = tap / a.KW;
-      kw = tap - kh * a.KW;
-    }
+    const int tap = k0 / a.Cin;
+    const int c0 = k0 - tap * a.Cin + kq * 4;
+    const int kh = tap / a.KW;
+    const int kw = tap - kh * a.KW;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int ih = aih[i] + kh;
       const int iw = aiw[i] + kw;
-      bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      if constexpr (STEM) ok = ok && (kw < a.KW);
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if (ok) {
         ra[i] = *(const f32x4*)(x + abase[i] + ((long long)ih * a.W + iw) * a.Cin + c0);
       } else {
@@ -177,12 +169,12 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(ConvArgs a) {
   }
 }
 
-template <int BM, int BN, bool STEM>
+template <int BM, int BN>
 static int launch_v1(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((conv_f32_kernel<BM, BN, STEM>), dim3((unsigned)nb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_f32_kernel<BM, BN>), dim3((unsigned)nb), dim3(256), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -196,16 +188,17 @@ static int conv_impl() {
 }
 
 int launch_conv_f32(const ConvArgs& a, hipStream_t s) {
-  const bool stem = (a.Cin == 4);
-  if (a.K % 32 != 0 || (!stem && a.Cin % 32 != 0) || (stem && (a.KWp != 8 || a.K != a.KH * 32))) {
+  // stem: dense padded RGB, see conv_f32_dma.hip (the only kernel that reads that layout)
+  const bool stem = (a.Cin == 3);
+  if ((stem && (!a.zero || a.KWp != 8 || a.KW != 7 || a.K != (a.KH * 24 + 15) / 16 * 16)) ||
+      (!stem && (a.K % 32 != 0 || a.Cin % 32 != 0))) {
     set_error("conv_f32: unsupported shape (K % 32, Cin % 32 or stem layout)");
     return EOSV_ERR_UNSUPPORTED;
   }
   const int impl = a.zero ? conv_impl() : 1;
-  if (impl == 1) {
-    if (stem) return launch_v1<128, 64, true>(a, s);
-    if (a.Cout <= 64) return launch_v1<128, 64, false>(a, s);
-    return launch_v1<128, 128, false>(a, s);
+  if (impl == 1 && !stem) {
+    if (a.Cout <= 64) return launch_v1<128, 64>(a, s);
+    return launch_v1<128, 128>(a, s);
   }
   return launch_conv_f32_dma(a, s, impl);
 }

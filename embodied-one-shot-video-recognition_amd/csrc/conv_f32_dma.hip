@@ -14,6 +14,14 @@
 //
 // Addressing is hoisted: each lane keeps, per staged row, the pointer of its (ih0, iw0)
 // pixel and the validity window; per K-step only a wave-uniform tap offset is added.
+//
+// Stem (Cin 3): the input is dense padded RGB, [N][H+2p][Wp][3] (Wp = W+2p rounded up to
+// even) with zero borders, and
+// K is laid out [kh][24] (kw*3 + c, 21 real + 3 zero weights) = 42 16-B chunks, padded to
+// 176 = 11 K-steps of 16: 84 % of the MFMA work is real (NHWC4 with kw padded to 8: 66 %).
+// A lane's chunk g = 4*kt + lc is kernel row g / 6, floats 4*(g % 6) .. +3 of that row's
+// 21-float tap run; the 16-B DMA source is then only 4-B aligned, which LDS-DMA accepts
+// (tests/native/dma_probe.cpp).  No bounds checks: the borders are real zeros.
 #include "common.h"
 
 namespace eosv {
@@ -33,7 +41,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   constexpr int BI = BN / (RPI * NW);
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile shape");
-  static_assert(!STEM || BK == 32, "stem needs one kernel row per K-step");
+  static_assert(!STEM || BK == 16, "stem chunk mapping assumes 4 chunks per K-step");
   __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
   static_assert(NS == 2 || NS == 3, "ring depth");
 
@@ -56,6 +64,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   // per staged A row: pointer at pixel (ih0, iw0) + this lane's logical chunk, and ih0/iw0
   const float* arow[AI];
   int aih[AI], aiw[AI];
+  const int xrow = ((a.W + 2 * a.pad + 1) & ~1) * 3;  // STEM: floats per padded input row
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
     const int row = wid * (BM / NW) + RPI * j + lr;
@@ -68,10 +77,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
       const int ow = rem - oh * a.Wo;
       aih[j] = oh * a.stride - a.pad;
       aiw[j] = ow * a.stride - a.pad;
-      // STEM: chunk = tap column kw (4 channels each); else chunk = 4 channels of the tap
-      const long long off = (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin;
-      arow[j] = x + off + (STEM ? (long long)lc * a.Cin : lc * 4);
-      if (STEM) aiw[j] += lc;  // this lane's tap column is kw = lc
+      if constexpr (STEM) {
+        // padded coordinates of tap (0, 0) are (oh*stride, ow*stride); aiw holds the chunk
+        aiw[j] = lc;
+        arow[j] = x + ((long long)img * (a.H + 2 * a.pad) + oh * a.stride) * xrow + (long long)ow * a.stride * 3;
+      } else {
+        arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 4;
+      }
     } else {
       aih[j] = -(1 << 28);
       aiw[j] = 0;
@@ -90,25 +102,30 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   auto stage = [&](int k0, int slot) {
     float* As = smem + slot * STAGE;
     float* Bs = As + BM * BK;
-    int kh, kw, c0;
     if constexpr (STEM) {
-      kh = k0 / BK;
-      kw = 0;
-      c0 = 0;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const int g = (k0 >> 2) + aiw[j];
+        const int kh = g / 6;
+        const bool ok = aih[j] > -(1 << 27) && kh < a.KH;
+        const float* src = ok ? arow[j] + kh * xrow + (g - 6 * kh) * 4 : zero;
+        float* dst = As + (wid * (BM / NW) + RPI * j) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
     } else {
       const int tap = k0 / a.Cin;
-      c0 = k0 - tap * a.Cin;
-      kh = tap / a.KW;
-      kw = tap - kh * a.KW;
-    }
-    const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;  // wave-uniform
+      const int c0 = k0 - tap * a.Cin;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+      const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;  // wave-uniform
 #pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      const int ih = aih[j] + kh, iw = aiw[j] + kw;
-      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const float* src = ok ? arow[j] + toff : zero;
-      float* dst = As + (wid * (BM / NW) + RPI * j) * BK;
-      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      for (int j = 0; j < AI; ++j) {
+        const int ih = aih[j] + kh, iw = aiw[j] + kw;
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const float* src = ok ? arow[j] + toff : zero;
+        float* dst = As + (wid * (BM / NW) + RPI * j) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
@@ -270,8 +287,8 @@ int launch_conv_f32_dma(const ConvArgs& a0, hipStream_t s, int variant) {
   }();
   ConvArgs a = a0;
   a.abl = abl;
-  const bool stem = (a.Cin == 4);
-  if (stem) return launch_dma<128, 64, 32, 2, 2, true>(a, s);
+  const bool stem = (a.Cin == 3);
+  if (stem) return launch_dma<128, 64, 16, 2, 2, true>(a, s);
   if (variant == 6) {  // BK 16, 2-deep ring, per-lane epilogue stores (pre-LDS-epilogue baseline)
     if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);
     return launch_dma<128, 128, 16, 2, 2, false, 2, false>(a, s);

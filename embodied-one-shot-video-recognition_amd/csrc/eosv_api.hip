@@ -4,7 +4,7 @@
 // (models.py:9-37): the ResNet layer plan (built from the arch id, torchvision v1.5
 // structure), BN folded into conv weights at load time, NHWC workspaces sized for
 // max_frames, and the per-chunk launch sequence
-//   pack NCHW->NHWC4 -> stem conv (+BN+ReLU) -> maxpool -> blocks (conv+BN[+ReLU],
+//   pack NCHW->padded RGB -> stem conv (+BN+ReLU) -> maxpool -> blocks (conv+BN[+ReLU],
 //   residual add + ReLU fused into the last conv's epilogue) -> avgpool.
 #include <hip/hip_bf16.h>
 
@@ -109,12 +109,13 @@ static int build_plan(eosv_handle* h) {
   }
   const int exp = bottleneck ? 4 : 1;
   h->D = 512 * exp;
-  // stem: 7x7/2 p3, Cin 3 padded to 4, kw padded to 8 -> K = 7*8*4 = 224
+  // stem: 7x7/2 p3 on dense padded RGB; K = [kh 7][24] (kw*3 + c, 3 zero weights per kh)
+  // padded to the kernel's K-step: f32 176 (BK 16), bf16 192 (BK 64)
   Conv st = make_conv(3, 64, 7, 2, 3, "convnet.0.weight", "convnet.1");
   st.stem = true;
   st.kwp = 8;
-  st.cinp = 4;
-  st.K = 7 * 8 * 4;
+  st.cinp = 3;
+  st.K = h->d.dtype == EOSV_BF16 ? 192 : 176;
   h->stem = st;
   h->hs = conv_out(h->d.height, 7, 2, 3);
   h->ws = conv_out(h->d.width, 7, 2, 3);
@@ -344,7 +345,7 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
                      bool bf, hipStream_t s) {
   const int H = h->d.height, W = h->d.width;
   int rc;
-  if ((rc = launch_pack_nchw_nhwc4(frames, B, H, W, h->pack, bf, s))) return rc;
+  if ((rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, bf, s))) return rc;
   if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, bufs[0], true, bf, s))) return rc;
   if ((rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s))) return rc;
   int hh = h->hp, ww = h->wp;
@@ -402,8 +403,10 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   int rc = build_plan(h);
   const size_t elt = desc->dtype == EOSV_BF16 ? 2 : 4;
   const size_t F = (size_t)desc->max_frames;
-  if (!rc) rc = dmalloc(h, &h->pack, F * desc->height * (desc->width + 2) * 4 * elt);
-  if (desc->dtype == EOSV_BF16) h->stem.K = 8 * 8 * 4;  // bf16 stem: 2 kernel rows per 64-deep K-step
+  const size_t pack_bytes = stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * elt;
+  if (!rc) rc = dmalloc(h, &h->pack, pack_bytes);
+  // zero borders of the padded stem input: written once here, the packer only fills interiors
+  if (!rc && hipMemset(h->pack, 0, pack_bytes) != hipSuccess) rc = (set_error("hipMemset pack"), EOSV_ERR_HIP);
   if (!rc) rc = dmalloc(h, &h->zero, 256);
   if (!rc && hipMemset(h->zero, 0, 256) != hipSuccess) rc = (set_error("hipMemset zero"), EOSV_ERR_HIP);
   for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);

@@ -1,8 +1,8 @@
 // Layout + pooling kernels around the conv stack (all HBM-bound byte movers).
 //
-//  pack_nchw_nhwc4 : the caller's [B,3,H,W] f32 frames (what network_test.py:58 hands
-//                    to self.mymodel) -> [B,H,W,4] with a zero 4th channel, so the
-//                    7x7 stem reads one 16-B pixel per tap (conv_f32.hip STEM path).
+//  pack_rgb_pad    : the caller's [B,3,H,W] f32 frames (what network_test.py:58 hands
+//                    to self.mymodel) -> dense padded RGB [B][H+2p][Wp][3] (f32 or bf16),
+//                    the layout the 7x7 stem reads (conv_f32_dma.hip / conv_bf16.hip).
 //  maxpool3x3s2    : torchvision conv1 -> bn1 -> relu -> maxpool(3,2,1) (convnet.3).
 //  avgpool         : AdaptiveAvgPool2d(1) + view(B,-1) (convnet.8, models.py:19-20):
 //                    sequential f32 sum over the HxW positions, then / (H*W).
@@ -17,40 +17,39 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN-preserving
 }
 
-__global__ void pack_nchw_nhwc4_kernel(const float* __restrict__ x, long long npix, int HW,
-                                       float4* __restrict__ y) {
+// one thread = one interior pixel; the zero borders of the padded image are written once
+// (eosv_create memsets the buffer) and never touched again
+template <typename T>
+__global__ void pack_rgb_pad_kernel(const float* __restrict__ x, long long npix, int H, int W, int pad, int Wp,
+                                    T* __restrict__ y) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
+  const int HW = H * W;
   const long long b = p / HW;
-  const long long hw = p - b * HW;
+  const int hw = (int)(p - b * HW);
+  const int yy = hw / W, xx = hw - (hw / W) * W;
   const float* src = x + b * 3 * HW + hw;
-  y[p] = make_float4(src[0], src[HW], src[2 * HW], 0.f);
+  T* dst = y + ((b * (H + 2 * pad) + yy + pad) * Wp + xx + pad) * 3;
+  if constexpr (sizeof(T) == 4) {
+    dst[0] = src[0];
+    dst[1] = src[HW];
+    dst[2] = src[2 * HW];
+  } else {
+    dst[0] = f2bf(src[0]);
+    dst[1] = f2bf(src[HW]);
+    dst[2] = f2bf(src[2 * HW]);
+  }
 }
 
-// bf16: rows shifted right by one pixel with zero borders, [B][H][W+2][4] (see conv_bf16.hip)
-__global__ void pack_nchw_nhwc4_bf16_kernel(const float* __restrict__ x, long long npix, int W, int HW,
-                                            ushort4* __restrict__ y) {
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npix) return;
-  const long long b = p / HW;
-  const long long hw = p - b * HW;
-  const long long row = p / W;  // = b*H + y
-  const int xx = (int)(p - row * W);
-  const float* src = x + b * 3 * HW + hw;
-  ushort4* dst = y + row * (W + 2);
-  dst[xx + 1] = make_ushort4(f2bf(src[0]), f2bf(src[HW]), f2bf(src[2 * HW]), 0);
-  if (xx == 0) dst[0] = make_ushort4(0, 0, 0, 0);
-  if (xx == W - 1) dst[W + 1] = make_ushort4(0, 0, 0, 0);
-}
-
-int launch_pack_nchw_nhwc4(const float* x, int B, int H, int W, void* y, int bf16, hipStream_t s) {
+int launch_pack_rgb_pad(const float* x, int B, int H, int W, int pad, void* y, int bf16, hipStream_t s) {
   const long long npix = (long long)B * H * W;
   const unsigned grid = (unsigned)((npix + 255) / 256);
+  const int Wp = stem_row_pixels(W, pad);
   if (bf16)
-    hipLaunchKernelGGL(pack_nchw_nhwc4_bf16_kernel, dim3(grid), dim3(256), 0, s, x, npix, W, H * W,
-                       (ushort4*)y);
+    hipLaunchKernelGGL(pack_rgb_pad_kernel<unsigned short>, dim3(grid), dim3(256), 0, s, x, npix, H, W, pad, Wp,
+                       (unsigned short*)y);
   else
-    hipLaunchKernelGGL(pack_nchw_nhwc4_kernel, dim3(grid), dim3(256), 0, s, x, npix, H * W, (float4*)y);
+    hipLaunchKernelGGL(pack_rgb_pad_kernel<float>, dim3(grid), dim3(256), 0, s, x, npix, H, W, pad, Wp, (float*)y);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

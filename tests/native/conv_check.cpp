@@ -12,12 +12,18 @@ using namespace eosv;
 static float frand(unsigned& s) { s = s * 1664525u + 1013904223u; return ((s >> 8) & 0xffff) / 32768.f - 1.f; }
 
 static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int pad, bool stem, bool res, bool relu) {
-  const int KWp = stem ? 8 : K, Cinp = stem ? 4 : Cin;
+  // stem: dense padded RGB input [N][H+2p][Wp][3] (zero borders), K = [kh][24] padded to 16
+  const int KWp = stem ? 8 : K, Cinp = Cin;
   const int Ho = (H + 2 * pad - K) / stride + 1, Wo = (W + 2 * pad - K) / stride + 1;
-  const int Kd = K * KWp * Cinp;
+  const int Kd = stem ? (K * 24 + 15) / 16 * 16 : K * KWp * Cinp;
+  const int Hx = stem ? H + 2 * pad : H, Wx = stem ? stem_row_pixels(W, pad) : W, off = stem ? pad : 0;
   unsigned s = 12345;
-  std::vector<float> x((size_t)N * H * W * Cinp), w((size_t)Cout * Kd, 0.f), b(Cout), r((size_t)N * Ho * Wo * Cout);
-  for (size_t i = 0; i < x.size(); ++i) x[i] = (stem && (i % 4 == 3)) ? 0.f : frand(s);
+  std::vector<float> x(stem ? stem_input_elems(N, H, W, pad) : (size_t)N * H * W * Cinp, 0.f),
+      w((size_t)Cout * Kd, 0.f), b(Cout), r((size_t)N * Ho * Wo * Cout);
+  for (int n = 0; n < N; ++n)
+    for (int i = 0; i < H; ++i)
+      for (int j = 0; j < W; ++j)
+        for (int c = 0; c < Cin; ++c) x[(((size_t)n * Hx + i + off) * Wx + j + off) * Cinp + c] = frand(s);
   for (int o = 0; o < Cout; ++o)
     for (int kh = 0; kh < K; ++kh)
       for (int kw = 0; kw < K; ++kw)
@@ -51,7 +57,7 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
               int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
               if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
               for (int c = 0; c < Cin; ++c)
-                acc += (double)x[(((size_t)n * H + ih) * W + iw) * Cinp + c] * w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c];
+                acc += (double)x[(((size_t)n * Hx + ih + off) * Wx + iw + off) * Cinp + c] * w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c];
             }
           size_t oi = (((size_t)n * Ho + oh) * Wo + ow) * Cout + o;
           if (res) acc += r[oi];
@@ -74,6 +80,7 @@ int main() {
   fails += check(3, 7, 7, 256, 512, 1, 2, 0, false, false, false);
   fails += check(1, 7, 7, 512, 512, 3, 1, 1, false, true, true);
   fails += check(2, 30, 30, 3, 64, 7, 2, 3, true, false, true);
+  fails += check(3, 37, 33, 3, 64, 7, 2, 3, true, false, true);  // odd sizes: row-width rounding, M tail
   fails += check(5, 1, 1, 512, 64, 1, 1, 0, false, false, false);
   printf("%d failures\n", fails);
   return fails;
