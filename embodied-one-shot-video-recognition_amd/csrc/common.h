@@ -49,6 +49,8 @@ struct ConvArgs {
 int launch_conv_f32(const ConvArgs& a, hipStream_t s);
 int launch_conv_f32_dma(const ConvArgs& a, hipStream_t s, int variant);
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
+bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
+int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ layout / pooling
 // stem input layout: zero-bordered RGB rows of stem_row_pixels(W, pad) pixels (even, so the

@@ -27,12 +27,15 @@ typedef unsigned short u16;
 __device__ __forceinline__ float bf_to_f(u16 v) { return __uint_as_float((unsigned)v << 16); }
 __device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
 
-template <int BM, int BN, int WM, int WN, bool STEM>
+// MF = MFMA tile edge: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16; same
+// cycles per FLOP, but the chip holds a higher clock on it with random operands)
+template <int BM, int BN, int WM, int WN, bool STEM, int MF>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BK = 64;  // bf16 elements per row = 128 B
   constexpr int NW = WM * WN;
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / WN / 32;
+  constexpr int TM = BM / WM / MF;
+  constexpr int TN = BN / WN / MF;
+  constexpr int ACC = MF * MF / 64;  // f32 accumulator elements per lane per tile
   constexpr int AI = BM / (8 * NW);
   constexpr int BI = BN / (8 * NW);
   constexpr int STAGE = (BM + BN) * BK;  // bf16 elements per ring slot
@@ -128,17 +131,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     }
   };
 
-  f32x16 acc[TM][TN];
+  typedef float accv __attribute__((ext_vector_type(ACC)));
+  accv acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+      for (int q = 0; q < ACC; ++q) acc[i][j][q] = 0.f;
 
-  const int h = lane >> 5;
-  const int r = lane & 31;
-  const int sw = (r >> 1) & 7;
+  // fragment lane map: row r = lane % MF, 16-B chunk q = lane / MF of the MFMA's k-slice
+  const int r = lane & (MF - 1);
+  const int q = lane / MF;
+  const int sw = (r >> 1) & 7;  // tile bases are multiples of 16 rows: the swizzle depends on r only
   const int nk = a.K / BK;
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -148,19 +153,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     if (kt + 1 < nk) stage((kt + 1) * BK, cur ^ 1);
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
+    constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int pch = ((2 * s + h) ^ sw) * 8;
+    for (int s = 0; s < BK / KS; ++s) {
+      const int pch = ((s * (KS / 8) + q) ^ sw) * 8;
       bf16x8 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(As + (wm * (BM / WM) + i * 32 + r) * BK + pch);
+      for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(As + (wm * (BM / WM) + i * MF + r) * BK + pch);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * 32 + r) * BK + pch);
+      for (int j = 0; j < TN; ++j) bf[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * MF + r) * BK + pch);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (MF == 32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -178,20 +188,25 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   float bcol[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * (BN / WN) + j * 32 + r;
+    const int n = n0 + wn * (BN / WN) + j * MF + r;
     bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
   }
   const int nthreads = 64 * NW;
+  constexpr int TPP = 32 / MF;  // MFMA row-tiles per 32-row pass
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  for (int i = 0; i < BM / WM / 32; ++i) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int t = 0; t < TPP; ++t)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int lrow = wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        ep[lrow * EPS + wn * (BN / WN) + j * 32 + r] = acc[i][j][q] + bcol[j];
-      }
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < ACC; ++e) {
+          // C/D maps: 32x32 row = (e&3) + 8(e>>2) + 4(lane>>5); 16x16 row = 4(lane>>4) + e
+          const int crow = MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * q : 4 * q + e;
+          const int lrow = wm * 32 + t * MF + crow;
+          ep[lrow * EPS + wn * (BN / WN) + j * MF + r] = acc[i * TPP + t][j][e] + bcol[j];
+        }
     __syncthreads();
     for (int idx = tid; idx < EPR * (BN / 8); idx += nthreads) {
       const int lrow = idx / (BN / 8);
@@ -227,12 +242,31 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   }
 }
 
+static int bf16_mfma() {
+  static int v = [] {
+    const char* e = getenv("EOSV_BF16_MFMA");  // 32 or 16 (A/B switch)
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+
+static int bf16_rows() {
+  static int v = [] {
+    const char* e = getenv("EOSV_BF16_ROWS");  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int BM, int BN, int WM, int WN, bool STEM>
 static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
+  if (bf16_mfma() == 32)
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 32>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -253,6 +287,7 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
+  if (bf16_rows() && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
   if (bf16_variant() == 3 && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
   if (bf16_variant() == 2) {  // 256x256 tiles, 8 waves of 128x64
     if (a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);

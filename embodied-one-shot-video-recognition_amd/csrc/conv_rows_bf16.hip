@@ -1,0 +1,276 @@
+// Row-strip direct 3x3 conv for ResNet stage 1 (bf16): Cin = Cout = 64, stride 1, pad 1,
+// 56-wide NHWC maps (every 3x3 conv of layer1 of ResNet-18/50 at 224x224 input).
+//
+// Why a second conv kernel: the implicit GEMM (conv_bf16.hip) re-reads every input pixel
+// from L2 once per tap (9x) and, with Cout = 64, its 128x64 tiles run at ~43 FLOP per byte
+// staged -- layer1 was 32 % of the bf16 forward at ~520 TF/s.  Here a persistent workgroup
+// (one per CU) keeps all 9 x 64 x 64 folded weights resident in LDS (72 KiB) and streams
+// the input as strips: the 6 padded input rows (58 x 64 ch) a strip of TR = 4 output rows
+// needs, double-buffered, so a strip's MFMA work (224 x 64 x 576) reads 44 KiB: ~370 FLOP
+// per staged byte.  A fragments are read straight from the staged rows: output pixel
+// (oy, ox) and tap (dy, dx) read staged row oy + dy, slot ox + dx.
+//
+// LDS (exactly 160 KiB): W [9 taps][64 cout][64 cin] | In[2][6 rows][58 slots][64 ch] (each
+// buffer padded to 44 KiB so the DMA pieces tile it).  128-B pixel / weight rows; 16-B chunk
+// c of input slot p stored at c ^ (p & 7), of weight row cout at c ^ ((cout >> 1) & 7) (XOR
+// applied on the DMA source).  Both make every ds_read_b128 fragment read conflict-free for
+// this kernel's pixel tiles, any tap (an input swizzle on p >> 1 cost 1.7x on the A reads).
+// 7 waves: wave w owns output-pixel tiles 2w, 2w+1 (16 px each, 224 per strip) x all 64
+// channels, v_mfma_f32_16x16x32_bf16.  Epilogue: acc + folded-BN shift (+ residual) + ReLU
+// staged through the strip's own input buffer in f32, two 32-channel passes, 16-B stores.
+//
+// Pipeline per strip: issue next strip's DMA (buffer cur^1) -> MFMAs on buffer cur ->
+// epilogue (exactly 4 global stores per lane, younger than the DMA) -> vmcnt(4) + barrier.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+
+namespace eosv {
+
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+constexpr int RW = 56;            // map width
+constexpr int TR = 4;             // output rows per strip
+constexpr int SLOTS = RW + 2;     // padded input row
+constexpr int NWAVE = 7;
+constexpr int NT = 64 * NWAVE;    // 448 threads
+constexpr int ROW_CHUNKS = SLOTS * 8;                   // 16-B chunks per staged row
+constexpr int IN_CHUNKS = (TR + 2) * ROW_CHUNKS;        // 2784
+constexpr int IN_PIECES = (IN_CHUNKS + 63) / 64;        // 44 DMA pieces of 1 KiB
+constexpr int IN_ELEMS = IN_PIECES * 512;               // bf16 elements per buffer (44 KiB)
+constexpr int W_ELEMS = 9 * 64 * 64;                    // 72 KiB
+constexpr int W_PIECES = W_ELEMS / 512;                 // 72
+constexpr int EPS = 36;                                 // f32 staging row stride (32 ch + 4)
+static_assert(W_ELEMS + 2 * IN_ELEMS == 163840 / 2, "LDS budget");
+static_assert(TR * RW == NWAVE * 2 * 16, "strip = 7 waves x 2 pixel tiles");
+static_assert(TR * RW * 4 == NT * 2, "two 16-B stores per thread per epilogue pass");
+static_assert(TR * RW * EPS * 4 <= IN_ELEMS * 2, "f32 staging fits one input buffer");
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)v << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
+
+// 16-B LDS read whose placement and wait the caller controls (see the k-step loop)
+__device__ __forceinline__ void ds_read16(bf16x8& v, const u16* p) {
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u16*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+}
+
+__device__ __forceinline__ void dma16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+}  // namespace
+
+__global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstrips) {
+  __shared__ __attribute__((aligned(16))) u16 smem[W_ELEMS + 2 * IN_ELEMS];
+  u16* Ws = smem;
+  u16* In = smem + W_ELEMS;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int H = a.H;
+  const int spi = H / TR;  // strips per image
+  const u16* __restrict__ x = (const u16*)a.x;
+  const u16* __restrict__ w = (const u16*)a.w;
+  const u16* zero = (const u16*)a.zero;
+
+  // resident weights: global [cout][tap*64 + c] -> LDS [tap][cout][chunk ^ swz(cout)]
+  for (int p = wid; p < W_PIECES; p += NWAVE) {
+    const int id = p * 64 + lane;  // 16-B chunk id in LDS order
+    const int row = id >> 3;       // tap * 64 + cout
+    const int tap = row >> 6, co = row & 63;
+    const int lc = (id & 7) ^ ((co >> 1) & 7);
+    dma16(w + (long long)co * a.K + tap * 64 + lc * 8, Ws + p * 512);
+  }
+  // input strip rows (y0-1 .. y0+4) of image img -> In[buf]; out-of-image rows/cols read zero
+  auto stage = [&](int strip, int buf) {
+    const int img = strip / spi;
+    const int y0 = (strip - img * spi) * TR;
+    const u16* ximg = x + (long long)img * H * RW * 64;
+    for (int p = wid; p < IN_PIECES; p += NWAVE) {
+      const int id = p * 64 + lane;
+      const int r = id / ROW_CHUNKS;
+      const int rem = id - r * ROW_CHUNKS;
+      const int slot = rem >> 3;
+      const int lc = (rem & 7) ^ (slot & 7);
+      const int iy = y0 - 1 + r, ix = slot - 1;
+      const bool ok = id < IN_CHUNKS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)RW;
+      dma16(ok ? ximg + ((long long)iy * RW + ix) * 64 + lc * 8 : zero, In + buf * IN_ELEMS + p * 512);
+    }
+  };
+
+  const int r16 = lane & 15;
+  const int q = lane >> 4;
+  // this lane's A-fragment pixels (one per pixel tile): staged (row oy, slot ox) at tap (0, 0)
+  int apix[2], aslot[2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int o = (2 * wid + mi) * 16 + r16;
+    const int oy = o / RW, ox = o - (o / RW) * RW;
+    apix[mi] = oy * SLOTS + ox;
+    aslot[mi] = ox;
+  }
+  float bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = a.bias ? a.bias[j * 16 + r16] : 0.f;
+
+  int strip = blockIdx.x;
+  if (strip < nstrips) stage(strip, 0);
+  // vmcnt(0) as the builtin (not asm) so the compiler's wait tracking knows the bias loads
+  // have landed and does not re-wait for them (draining the in-flight DMA) inside the loop
+  __builtin_amdgcn_s_waitcnt(0x0f70);
+  __builtin_amdgcn_s_barrier();
+
+  u16* __restrict__ y = (u16*)a.y;
+  const u16* __restrict__ res = (const u16*)a.res;
+  for (int k = 0; strip < nstrips; ++k, strip += gridDim.x) {
+    const int cur = k & 1;
+    const int next = strip + gridDim.x;
+    if (next < nstrips) stage(next, cur ^ 1);
+    const u16* Ib = In + cur * IN_ELEMS;
+    const int img = strip / spi;
+    const int y0 = (strip - img * spi) * TR;
+    const long long obase = ((long long)img * H + y0) * RW * 64;  // strip's first output pixel
+    // Residual for the epilogue, loaded now so the MFMA phase hides its latency.  Inline-asm
+    // loads: with an LDS-DMA in flight hipcc waits vmcnt(0) before every use of an ordinary
+    // load's result (and here even before issuing one), which would drain the prefetch.
+    uint4 rv[4];
+    if (res) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int idx = tid + (t & 1) * NT;
+        const u16* src = res + obase + (long long)(idx >> 2) * 64 + (t >> 1) * 32 + (idx & 3) * 8;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv[t]) : "v"(src) : "memory");
+      }
+    }
+
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[mi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // 18 k-steps (9 taps x two 32-deep slices).  Fragments double-buffered in registers: the
+    // next step's 6 ds_reads are issued (inline asm, so hipcc can neither sink them next to
+    // their MFMAs nor wait lgkmcnt(0) per read) ahead of this step's 8 MFMAs, and one
+    // lgkmcnt(0) per step retires them; sched_barrier keeps each step's MFMAs inside it.
+    bf16x8 af[2][2], bf[2][4];
+    auto frags = [&](int t, int b) {
+      const int tap = t >> 1, dy = tap / 3, dx = tap - (tap / 3) * 3;
+      const int lc = 4 * (t & 1) + q;  // this lane's 16-B chunk of the 32-deep k-slice
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int pix = apix[mi] + dy * SLOTS + dx;
+        ds_read16(af[b][mi], Ib + pix * 64 + ((lc ^ ((aslot[mi] + dx) & 7)) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = j * 16 + r16;
+        ds_read16(bf[b][j], Ws + (tap * 64 + co) * 64 + ((lc ^ ((co >> 1) & 7)) * 8));
+      }
+    };
+    frags(0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 18; ++t) {
+      if (t + 1 < 18) frags(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);  // the reads go out before this step's MFMAs
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t & 1][mi], bf[t & 1][j], acc[mi][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // ... and the wait after all of them
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // epilogue, staged through buffer cur (its A reads are done after this barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float* ep = (float*)(In + cur * IN_ELEMS);
+    if (res) {
+      // the asm loads above (and the prefetch DMA, issued before them) have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
+    }
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int o = (2 * wid + mi) * 16 + 4 * q + e;  // 16x16 C/D: row 4(lane>>4) + e
+            ep[o * EPS + jj * 16 + r16] = acc[mi][2 * pass + jj][e] + bias[2 * pass + jj];
+          }
+      // raw barrier: __syncthreads() would also drain the in-flight DMA (vmcnt(0))
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int idx = tid + t * NT;  // 224 px x 4 chunks of 8 channels
+        const int o = idx >> 2, c8 = idx & 3;
+        const f32x4 v0 = *(const f32x4*)(ep + o * EPS + c8 * 8);
+        const f32x4 v1 = *(const f32x4*)(ep + o * EPS + c8 * 8 + 4);
+        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const long long off = obase + (long long)o * 64 + pass * 32 + c8 * 8;
+        if (res) {
+          const uint4 r4 = rv[pass * 2 + t];
+          const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[2 * i] += bf2f((u16)(ru[i] & 0xffff));
+            v[2 * i + 1] += bf2f((u16)(ru[i] >> 16));
+          }
+        }
+        unsigned pk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float lo = v[2 * i], hi = v[2 * i + 1];
+          if (a.relu) {
+            lo = fmaxf(lo, 0.f);
+            hi = fmaxf(hi, 0.f);
+          }
+          pk[i] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+        }
+        *(uint4*)(y + off) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    // next strip's DMA (issued before this strip's 4 stores per lane) must have landed
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// shapes this kernel takes (everything else stays on the implicit GEMM)
+bool conv_rows_bf16_ok(const ConvArgs& a) {
+  return a.Cin == 64 && a.Cout == 64 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.W == RW &&
+         a.H % TR == 0 && a.Ho == a.H && a.Wo == a.W && a.K == 9 * 64 && a.zero;
+}
+
+int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s) {
+  static int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev))
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const long long nstrips = (long long)a.N * (a.H / TR);
+  if (nstrips <= 0) return EOSV_OK;
+  if (nstrips > 0x7fffffffLL) return set_error("conv_rows: too many strips"), EOSV_ERR_UNSUPPORTED;
+  const unsigned grid = (unsigned)std::min<long long>(nstrips, ncu);
+  hipLaunchKernelGGL(conv_rows_bf16_kernel, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+}  // namespace eosv

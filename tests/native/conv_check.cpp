@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "common.h"
 
@@ -72,8 +73,87 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
   return bad ? 1 : 0;
 }
 
+static unsigned short f2bf(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+static float bf2f(unsigned short v) {
+  unsigned u = (unsigned)v << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// bf16 3x3/s1/p1 conv through launch_conv_bf16 (stage-1 shapes take the row-strip kernel);
+// reference in double on the bf16-rounded operands, checked on images `checked` only
+static int check_bf16(int N, int H, int W, int C, bool res, bool relu) {
+  const int K = 9 * C;
+  unsigned s = 777;
+  std::vector<unsigned short> x((size_t)N * H * W * C), w((size_t)C * K), r((size_t)N * H * W * C);
+  std::vector<float> b(C);
+  for (auto& v : x) v = f2bf(frand(s));
+  for (auto& v : w) v = f2bf(frand(s) * 0.1f);
+  for (auto& v : r) v = f2bf(frand(s));
+  for (auto& v : b) v = frand(s);
+  unsigned short *dx, *dw, *dr, *dy;
+  float* db;
+  void* dz;
+  hipMalloc(&dx, x.size() * 2); hipMalloc(&dw, w.size() * 2); hipMalloc(&dr, r.size() * 2);
+  hipMalloc(&dy, r.size() * 2); hipMalloc(&db, C * 4); hipMalloc(&dz, 256); hipMemset(dz, 0, 256);
+  hipMemcpy(dx, x.data(), x.size() * 2, hipMemcpyHostToDevice);
+  hipMemcpy(dw, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  hipMemcpy(dr, r.data(), r.size() * 2, hipMemcpyHostToDevice);
+  hipMemcpy(db, b.data(), C * 4, hipMemcpyHostToDevice);
+  hipMemset(dy, 0xff, r.size() * 2);
+  ConvArgs a{};
+  a.x = dx; a.w = dw; a.bias = db; a.res = res ? dr : nullptr; a.y = dy;
+  a.N = N; a.H = H; a.W = W; a.Cin = C; a.Ho = H; a.Wo = W; a.Cout = C;
+  a.KH = 3; a.KW = 3; a.KWp = 3; a.stride = 1; a.pad = 1; a.K = K; a.relu = relu; a.zero = dz;
+  const int rc = launch_conv_bf16(a, 0);
+  hipDeviceSynchronize();
+  std::vector<unsigned short> y(r.size());
+  hipMemcpy(y.data(), dy, y.size() * 2, hipMemcpyDeviceToHost);
+  const int checked[4] = {0, 1, N - 2, N - 1};
+  double maxerr = 0;
+  long bad = 0;
+  for (int ci = 0; ci < 4; ++ci) {
+    const int n = checked[ci];
+    for (int oh = 0; oh < H; ++oh)
+      for (int ow = 0; ow < W; ++ow)
+        for (int o = 0; o < C; ++o) {
+          double acc = b[o];
+          for (int kh = 0; kh < 3; ++kh)
+            for (int kw = 0; kw < 3; ++kw) {
+              const int ih = oh - 1 + kh, iw = ow - 1 + kw;
+              if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+              for (int c = 0; c < C; ++c)
+                acc += (double)bf2f(x[(((size_t)n * H + ih) * W + iw) * C + c]) *
+                       bf2f(w[(size_t)o * K + (kh * 3 + kw) * C + c]);
+            }
+          const size_t oi = (((size_t)n * H + oh) * W + ow) * C + o;
+          if (res) acc += bf2f(r[oi]);
+          if (relu && acc < 0) acc = 0;
+          const double e = fabs(acc - bf2f(y[oi]));
+          if (e > 1e-2 * (1 + fabs(acc))) {
+            if (bad < 5) printf("  bad n%d oh%d ow%d o%d ref %f got %f\n", n, oh, ow, o, acc, bf2f(y[oi]));
+            ++bad;
+          }
+          maxerr = fmax(maxerr, e);
+        }
+  }
+  printf("%s bf16 N%d H%d W%d C%d res%d relu%d rc=%d maxerr %.3e bad %ld\n", bad ? "FAIL" : "ok  ", N, H, W, C, res,
+         relu, rc, maxerr, bad);
+  hipFree(dx); hipFree(dw); hipFree(dr); hipFree(dy); hipFree(db); hipFree(dz);
+  return bad || rc ? 1 : 0;
+}
+
 int main() {
   int fails = 0;
+  // stage-1 shape (row-strip kernel): 300 images = 4200 strips, several strips per workgroup
+  fails += check_bf16(300, 56, 56, 64, true, true);
+  fails += check_bf16(3, 56, 56, 64, false, true);
   fails += check(1, 8, 8, 32, 64, 1, 1, 0, false, false, false);
   fails += check(2, 9, 7, 64, 64, 3, 1, 1, false, false, false);
   fails += check(2, 14, 14, 64, 128, 3, 2, 1, false, true, true);
