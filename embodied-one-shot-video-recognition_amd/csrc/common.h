@@ -49,13 +49,16 @@ struct ConvArgs {
 int launch_conv_f32(const ConvArgs& a, hipStream_t s);
 int launch_conv_f32_dma(const ConvArgs& a, hipStream_t s, int variant);
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
+bool stem_pool_bf16_ok(int H, int W);  // stem_pool_bf16.hip: fused stem conv + ReLU + maxpool
+int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
+                          hipStream_t s);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ layout / pooling
 // stem input layout: zero-bordered RGB rows of stem_row_pixels(W, pad) pixels (even, so the
 // stem's bf16 DMA sources stay 4-B aligned)
-inline int stem_row_pixels(int W, int pad) { return (W + 2 * pad + 1) & ~1; }
+__host__ __device__ inline int stem_row_pixels(int W, int pad) { return (W + 2 * pad + 1) & ~1; }
 inline size_t stem_input_elems(int B, int H, int W, int pad) {
   return (size_t)B * (H + 2 * pad) * stem_row_pixels(W, pad) * 3 + 64;  // + over-read slack
 }

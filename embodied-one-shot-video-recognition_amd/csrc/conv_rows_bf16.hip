@@ -16,11 +16,13 @@
 // applied on the DMA source).  Both make every ds_read_b128 fragment read conflict-free for
 // this kernel's pixel tiles, any tap (an input swizzle on p >> 1 cost 1.7x on the A reads).
 // 7 waves: wave w owns output-pixel tiles 2w, 2w+1 (16 px each, 224 per strip) x all 64
-// channels, v_mfma_f32_16x16x32_bf16.  Epilogue: acc + folded-BN shift (+ residual) + ReLU
-// staged through the strip's own input buffer in f32, two 32-channel passes, 16-B stores.
+// channels, v_mfma_f32_16x16x32_bf16 computing D = W . X^T so that a lane ends up holding 4
+// adjacent channels of one pixel.  Epilogue from registers: acc + folded-BN shift
+// (+ residual) + ReLU, 8-B stores; no LDS staging, no epilogue barriers.
 //
-// Pipeline per strip: issue next strip's DMA (buffer cur^1) -> MFMAs on buffer cur ->
-// epilogue (exactly 4 global stores per lane, younger than the DMA) -> vmcnt(4) + barrier.
+// Pipeline per strip: issue next strip's DMA (buffer cur^1) and this strip's residual loads
+// -> MFMAs on buffer cur -> epilogue (exactly 8 global stores per lane, younger than the
+// DMA) -> vmcnt(8) + barrier.
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -43,11 +45,8 @@ constexpr int IN_PIECES = (IN_CHUNKS + 63) / 64;        // 44 DMA pieces of 1 Ki
 constexpr int IN_ELEMS = IN_PIECES * 512;               // bf16 elements per buffer (44 KiB)
 constexpr int W_ELEMS = 9 * 64 * 64;                    // 72 KiB
 constexpr int W_PIECES = W_ELEMS / 512;                 // 72
-constexpr int EPS = 36;                                 // f32 staging row stride (32 ch + 4)
 static_assert(W_ELEMS + 2 * IN_ELEMS == 163840 / 2, "LDS budget");
 static_assert(TR * RW == NWAVE * 2 * 16, "strip = 7 waves x 2 pixel tiles");
-static_assert(TR * RW * 4 == NT * 2, "two 16-B stores per thread per epilogue pass");
-static_assert(TR * RW * EPS * 4 <= IN_ELEMS * 2, "f32 staging fits one input buffer");
 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)v << 16); }
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
@@ -85,20 +84,32 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     const int lc = (id & 7) ^ ((co >> 1) & 7);
     dma16(w + (long long)co * a.K + tap * 64 + lc * 8, Ws + p * 512);
   }
-  // input strip rows (y0-1 .. y0+4) of image img -> In[buf]; out-of-image rows/cols read zero
+  // Input strip rows (y0-1 .. y0+4) -> In[buf]; out-of-image rows / pad columns read zero.
+  // The chunk -> (staged row, source offset) map is the same for every strip: precomputed.
+  constexpr int PPW = (IN_PIECES + NWAVE - 1) / NWAVE;  // DMA pieces per wave (6 or 7)
+  int goff[PPW], grow[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int id = (wid + NWAVE * i) * 64 + lane;
+    const int r = id / ROW_CHUNKS;
+    const int rem = id - r * ROW_CHUNKS;
+    const int slot = rem >> 3;
+    const int lc = (rem & 7) ^ (slot & 7);
+    const bool colok = id < IN_CHUNKS && slot >= 1 && slot <= RW;
+    goff[i] = ((r - 1) * RW + (slot - 1)) * 64 + lc * 8;  // from pixel (y0, 0)
+    grow[i] = colok ? r : -1000;
+  }
   auto stage = [&](int strip, int buf) {
     const int img = strip / spi;
     const int y0 = (strip - img * spi) * TR;
-    const u16* ximg = x + (long long)img * H * RW * 64;
-    for (int p = wid; p < IN_PIECES; p += NWAVE) {
-      const int id = p * 64 + lane;
-      const int r = id / ROW_CHUNKS;
-      const int rem = id - r * ROW_CHUNKS;
-      const int slot = rem >> 3;
-      const int lc = (rem & 7) ^ (slot & 7);
-      const int iy = y0 - 1 + r, ix = slot - 1;
-      const bool ok = id < IN_CHUNKS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)RW;
-      dma16(ok ? ximg + ((long long)iy * RW + ix) * 64 + lc * 8 : zero, In + buf * IN_ELEMS + p * 512);
+    const u16* xs = x + ((long long)img * H + y0) * RW * 64;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wid + NWAVE * i;
+      if (p < IN_PIECES) {
+        const bool ok = (unsigned)(y0 - 1 + grow[i]) < (unsigned)H;
+        dma16(ok ? xs + goff[i] : zero, In + buf * IN_ELEMS + p * 512);
+      }
     }
   };
 
@@ -113,9 +124,10 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     apix[mi] = oy * SLOTS + ox;
     aslot[mi] = ox;
   }
-  float bias[4];
+  // D = W . X^T per tile: a lane's 4 accumulators are couts j*16 + 4q .. +3 of pixel r16
+  f32x4 bias[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bias[j] = a.bias ? a.bias[j * 16 + r16] : 0.f;
+  for (int j = 0; j < 4; ++j) bias[j] = a.bias ? *(const f32x4*)(a.bias + j * 16 + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
 
   int strip = blockIdx.x;
   if (strip < nstrips) stage(strip, 0);
@@ -137,14 +149,15 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     // Residual for the epilogue, loaded now so the MFMA phase hides its latency.  Inline-asm
     // loads: with an LDS-DMA in flight hipcc waits vmcnt(0) before every use of an ordinary
     // load's result (and here even before issuing one), which would drain the prefetch.
-    uint4 rv[4];
+    uint2 rv[2][4];
     if (res) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int idx = tid + (t & 1) * NT;
-        const u16* src = res + obase + (long long)(idx >> 2) * 64 + (t >> 1) * 32 + (idx & 3) * 8;
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv[t]) : "v"(src) : "memory");
-      }
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u16* src = res + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q;
+          asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(rv[mi][j]) : "v"(src) : "memory");
+        }
     }
 
     f32x4 acc[2][4];
@@ -183,69 +196,42 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t & 1][mi], bf[t & 1][j], acc[mi][j], 0, 0, 0);
+          acc[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[t & 1][j], af[t & 1][mi], acc[mi][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // ... and the wait after all of them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // epilogue, staged through buffer cur (its A reads are done after this barrier)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    float* ep = (float*)(In + cur * IN_ELEMS);
+    // Epilogue straight from registers: per (pixel tile, cout tile) a lane owns 4 adjacent
+    // channels of one pixel -> one 8-B store (16 lanes x 32 B per pixel row per instruction).
     if (res) {
       // the asm loads above (and the prefetch DMA, issued before them) have landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
     }
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int o = (2 * wid + mi) * 16 + 4 * q + e;  // 16x16 C/D: row 4(lane>>4) + e
-            ep[o * EPS + jj * 16 + r16] = acc[mi][2 * pass + jj][e] + bias[2 * pass + jj];
-          }
-      // raw barrier: __syncthreads() would also drain the in-flight DMA (vmcnt(0))
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int idx = tid + t * NT;  // 224 px x 4 chunks of 8 channels
-        const int o = idx >> 2, c8 = idx & 3;
-        const f32x4 v0 = *(const f32x4*)(ep + o * EPS + c8 * 8);
-        const f32x4 v1 = *(const f32x4*)(ep + o * EPS + c8 * 8 + 4);
-        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        const long long off = obase + (long long)o * 64 + pass * 32 + c8 * 8;
+        for (int e = 0; e < 4; ++e) v[e] = acc[mi][j][e] + bias[j][e];
         if (res) {
-          const uint4 r4 = rv[pass * 2 + t];
-          const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[2 * i] += bf2f((u16)(ru[i] & 0xffff));
-            v[2 * i + 1] += bf2f((u16)(ru[i] >> 16));
-          }
+          v[0] += bf2f((u16)(rv[mi][j].x & 0xffff));
+          v[1] += bf2f((u16)(rv[mi][j].x >> 16));
+          v[2] += bf2f((u16)(rv[mi][j].y & 0xffff));
+          v[3] += bf2f((u16)(rv[mi][j].y >> 16));
         }
-        unsigned pk[4];
+        if (a.relu)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float lo = v[2 * i], hi = v[2 * i + 1];
-          if (a.relu) {
-            lo = fmaxf(lo, 0.f);
-            hi = fmaxf(hi, 0.f);
-          }
-          pk[i] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
-        }
-        *(uint4*)(y + off) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+        const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        *(uint2*)(y + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q) = make_uint2(lo, hi);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    // next strip's DMA (issued before this strip's 4 stores per lane) must have landed
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // next strip's DMA (issued before this strip's 8 stores per lane) must have landed, and
+    // every wave's reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -340,14 +340,38 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
   return EOSV_OK;
 }
 
+static bool stem_pool_fused() {
+  static const bool v = [] {
+    const char* e = getenv("EOSV_BF16_STEMPOOL");  // 0 = separate stem conv + maxpool (A/B switch)
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 // stem -> maxpool -> stage-0 blocks for frames [0, B) of `frames`, output into `dst`
 static int run_front(eosv_handle* h, const float* frames, int B, void* const* bufs, void* dst, void** xout,
                      bool bf, hipStream_t s) {
   const int H = h->d.height, W = h->d.width;
   int rc;
   if ((rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, bf, s))) return rc;
-  if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, bufs[0], true, bf, s))) return rc;
-  if ((rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s))) return rc;
+  if (bf && stem_pool_fused() && stem_pool_bf16_ok(H, W)) {
+    // fused stem conv + ReLU + maxpool (profiled as the stem layer)
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->prof) {
+      e0 = prof_event(h);
+      e1 = prof_event(h);
+      if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
+      EOSV_HIP_CHECK(hipEventRecord(e0, s));
+    }
+    if ((rc = launch_stem_pool_bf16(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s))) return rc;
+    if (h->prof) {
+      EOSV_HIP_CHECK(hipEventRecord(e1, s));
+      h->recs.push_back({h->stem.id, e0, e1, 2.0 * B * h->hs * h->ws * 64 * 147});
+    }
+  } else {
+    if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, bufs[0], true, bf, s))) return rc;
+    if ((rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s))) return rc;
+  }
   int hh = h->hp, ww = h->wp;
   return run_blocks(h, 0, h->n_front, bufs[1], bufs, B, hh, ww, dst, xout, bf, s);
 }
@@ -403,10 +427,13 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   int rc = build_plan(h);
   const size_t elt = desc->dtype == EOSV_BF16 ? 2 : 4;
   const size_t F = (size_t)desc->max_frames;
-  const size_t pack_bytes = stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * elt;
-  if (!rc) rc = dmalloc(h, &h->pack, pack_bytes);
+  // + 256 B: the fused bf16 stem's DMA reads up to 12 B before a row (stem_pool_bf16.hip)
+  const size_t pack_bytes = stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * elt + 256;
+  void* pack_base = nullptr;
+  if (!rc) rc = dmalloc(h, &pack_base, pack_bytes);
   // zero borders of the padded stem input: written once here, the packer only fills interiors
-  if (!rc && hipMemset(h->pack, 0, pack_bytes) != hipSuccess) rc = (set_error("hipMemset pack"), EOSV_ERR_HIP);
+  if (!rc && hipMemset(pack_base, 0, pack_bytes) != hipSuccess) rc = (set_error("hipMemset pack"), EOSV_ERR_HIP);
+  if (!rc) h->pack = (char*)pack_base + 128;
   if (!rc) rc = dmalloc(h, &h->zero, 256);
   if (!rc && hipMemset(h->zero, 0, 256) != hipSuccess) rc = (set_error("hipMemset zero"), EOSV_ERR_HIP);
   for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);

@@ -1,0 +1,228 @@
+// Fused ResNet stem for bf16: conv 7x7/2 p3 (3 -> 64, folded BN) + ReLU + maxpool 3x3/2 p1,
+// torchvision's convnet.0-3 (reference models.py:19 via self.convnet).
+//
+// The unfused pair wrote the 112 x 112 x 64 stem map (1.6 MB per frame) to HBM and read it
+// back for the pool; with K = 147 the stem itself is a short-K implicit GEMM that ran at
+// ~280 TF/s.  Here one workgroup walks one image top to bottom:
+//  * wave t owns pooled columns 7t .. 7t+6, i.e. the 16 stem columns 14t-1 .. 14t+14 (one
+//    MFMA pixel tile; column 14t+14 is computed and dropped);
+//  * all 64 x 192 folded stem weights live in registers (24 A fragments per lane), so the
+//    k-loop only reads input pixels from LDS;
+//  * per pooled row py the wave computes stem rows 2py and 2py+1 (row 2py-1 is kept from the
+//    previous step), takes the row max and then the column max (DPP row shifts) of the raw
+//    accumulators, and only then adds the BN shift, applies ReLU and rounds to bf16 for the
+//    7 pooled pixels x 64 channels it stores (all three are monotone, so they commute with
+//    max: the same values as stem conv -> bf16 -> maxpool up to f32 summation order).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 with D = W . X^T (rows = output channels, columns = stem
+// pixels), K = [kh 8][24] (kw*3 + c, 21 real; kh 7 and the 3 spare k of each row carry zero
+// weights), 6 k-slices of 32.  A B-fragment chunk (8 consecutive k of one kernel row) is 8
+// consecutive bf16 of a padded input row starting at byte 12*sx + 16*c: only 4-B aligned,
+// so LDS holds every input row 4 times, copy m shifted by 4m bytes so that the
+// lanes with sx = m (mod 4) read it with an aligned ds_read_b128.
+//
+// LDS: a ring of 16 padded input rows x 4 copies (row r in slot (r + 3) & 15, so the 4 rows
+// a step prefetches are contiguous); LDS-DMA from the dense padded RGB pack (4-B aligned
+// sources).  Step py needs input rows 4py .. 4py+8 and prefetches 4py+9 .. 4py+12.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+
+namespace eosv {
+
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+constexpr int MAX_TILES = 8;                         // pooled width <= 56 (input width <= 224): 2 waves/SIMD
+constexpr int KSTEM = 192;                           // [kh 8][24]
+constexpr int RING = 16;
+
+__host__ __device__ constexpr int copy_chunks(int ntiles) {
+  // bytes a copy must hold: 12 * (largest sx + 1) + 12 (shift) + 48 (3 chunks of a kernel row)
+  return (12 * (14 * ntiles) + 12 + 48 + 15) / 16;
+}
+constexpr int LDS_BYTES = RING * 4 * copy_chunks(MAX_TILES) * 16;
+
+__device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
+
+__device__ __forceinline__ void dma16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// value of the lane `sh` positions up within its 16-lane row (DPP row_shl); 0 past the row end
+__device__ __forceinline__ float row_shl(float v, int sh) {
+  const int iv = __float_as_int(v);
+  const int r = sh == 1 ? __builtin_amdgcn_update_dpp(0, iv, 0x101, 0xf, 0xf, false)
+                        : __builtin_amdgcn_update_dpp(0, iv, 0x102, 0xf, 0xf, false);
+  return __int_as_float(r);
+}
+}  // namespace
+
+// x: padded bf16 RGB [N][H+6][Wp][3] (stem_row_pixels), w: [64][192] bf16, bias [64] f32,
+// y: [N][Hq][Wq][64] bf16 (pooled).  Grid = N images, block = 64 * ntiles threads.
+__global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u16* __restrict__ x,
+                                                                       const u16* __restrict__ w,
+                                                                       const float* __restrict__ bias, u16* y,
+                                                                       int H, int W, int Hs, int Ws, int Hq, int Wq) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[LDS_BYTES];
+  const int ntiles = blockDim.x >> 6;
+  const int CH = copy_chunks(ntiles);  // 16-B chunks per copy
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int r16 = lane & 15;
+  const int q = lane >> 4;
+  const int img = blockIdx.x;
+  const int Wp = stem_row_pixels(W, 3);
+  const int rowbytes = Wp * 6;
+  const int Hpad = H + 6;
+  const unsigned char* ximg = (const unsigned char*)(x + (long long)img * Hpad * Wp * 3);
+
+  // weights -> registers: A fragment (j, s) = couts j*16 + r16, k = 32s + 8q .. +7
+  bf16x8 wf[4][6];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) wf[j][s] = *(const bf16x8*)(w + (j * 16 + r16) * KSTEM + 32 * s + 8 * q);
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(bias + j * 16 + 4 * q);
+
+  // DMA of input rows [r0, r0 + nrows) (nrows * 4 copies * CH chunks, lane-linear from the
+  // ring slot of r0); rows past the padded image are clamped (their results are discarded)
+  auto stage = [&](int r0, int nrows) {
+    const int total = nrows * 4 * CH;
+    unsigned char* dst0 = ring + (size_t)(((r0 + 3) & (RING - 1)) * 4) * CH * 16;
+    for (int p = wid; p * 64 < total; p += ntiles) {
+      const int id = p * 64 + lane;
+      const int rr = id / (4 * CH);
+      const int rem = id - rr * 4 * CH;
+      const int m = rem / CH;
+      const int c = rem - m * CH;
+      const int row = min(r0 + rr, Hpad - 1);
+      const unsigned char* src = ximg + (long long)row * rowbytes + 16 * c - ((4 * m) & 15);
+      if (id < total) dma16(src, dst0 + (size_t)p * 1024);  // EXEC-masked: no write past the region
+    }
+  };
+
+  // this lane's stem column and its copy / byte offset inside a ring row
+  const int sx = 14 * wid - 1 + r16;
+  const int m = sx & 3;
+  const bool colok = sx >= 0 && sx < Ws;
+  // 16-B chunk index of this lane's pixel in its copy (12*sx + shift is a multiple of 16);
+  // indexing whole chunks lets the compiler emit ds_read_b128 (a byte offset it cannot
+  // prove aligned becomes 2 x ds_read2_b32)
+  const int xchunk = m * CH + (12 * sx + ((4 * m) & 15)) / 16;
+
+  auto stem_row = [&](int sy, f32x4 (&acc)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int g = 4 * s + q;        // chunk of the [kh][24] K layout
+      const int kh = min(g / 3, 6);   // kh 7: zero weights, any finite pixel
+      const int c = g - 3 * (g / 3);
+      const int slot = (2 * sy + kh + 3) & (RING - 1);
+      const bf16x8 xf = ((const bf16x8*)ring)[slot * 4 * CH + xchunk + c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xf, acc[j], 0, 0, 0);
+    }
+  };
+  // Per step a wave DMAs its share of 4 rows x 4 copies (pieces p = wid + ntiles*i of the
+  // step's contiguous ring region); the chunk -> (row, source offset) map is fixed: precomputed.
+  constexpr int PPW = 4;  // >= ceil(16 * CH / 64 / ntiles) for every ntiles <= MAX_TILES
+  int prr[PPW], pcoff[PPW];
+  const int step_chunks = 16 * CH;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int id = (wid + ntiles * i) * 64 + lane;
+    const int rr = id / (4 * CH);
+    const int rem = id - rr * 4 * CH;
+    const int mm = rem / CH;
+    const int c = rem - mm * CH;
+    prr[i] = id < step_chunks ? rr : -1;
+    pcoff[i] = 16 * c - ((4 * mm) & 15);
+  }
+  auto stage4 = [&](int r0) {
+    unsigned char* dst0 = ring + (size_t)(((r0 + 3) & (RING - 1)) * 4) * CH * 16;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wid + ntiles * i;
+      if (prr[i] >= 0) {  // EXEC-masked: no write past the region
+        const int row = min(r0 + prr[i], Hpad - 1);
+        dma16(ximg + (long long)row * rowbytes + pcoff[i], dst0 + (size_t)p * 1024);
+      }
+    }
+  };
+
+  stage(0, 13);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // The pool runs on the raw accumulators: max over the window commutes with + shift, ReLU and
+  // the bf16 rounding (all monotone), so only the 7 pooled values per channel get them.
+  // Stem pixels outside the map enter as -inf (maxpool's padding).
+  const float NEG = -INFINITY;
+  f32x4 prev[4];  // stem row 2py - 1
+#pragma unroll
+  for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
+  u16* yimg = y + (long long)img * Hq * Wq * 64;
+  const int px = 7 * wid + (r16 >> 1);  // pooled column this lane writes (even r16 <= 12)
+  const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
+
+  for (int py = 0; py < Hq; ++py) {
+    if (py + 1 < Hq) stage4(4 * py + 9);
+    f32x4 a1[4], a2[4];
+    stem_row(2 * py, a1);
+    stem_row(2 * py + 1, a2);
+    const bool ok1 = colok && 2 * py < Hs, ok2 = colok && 2 * py + 1 < Hs;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      unsigned pk[2];
+#pragma unroll
+      for (int e2 = 0; e2 < 2; ++e2) {
+        float o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * e2 + h;
+          const float v2 = ok2 ? a2[j][e] : NEG;
+          const float v = fmaxf(fmaxf(prev[j][e], ok1 ? a1[j][e] : NEG), v2);  // row max
+          prev[j][e] = v2;
+          // column max: pooled column i of this tile = stem columns r16 = 2i, 2i+1, 2i+2
+          const float c = fmaxf(fmaxf(v, row_shl(v, 1)), row_shl(v, 2));
+          o[h] = fmaxf(c + bv[j][e], 0.f);
+        }
+        pk[e2] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+      }
+      if (writer) *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk[0], pk[1]);
+    }
+    // next step's rows have landed (their DMA is older than this step's 4 stores) and every
+    // wave is done reading the slots the step after will overwrite
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool stem_pool_bf16_ok(int H, int W) {
+  const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
+  const int Wq = (Ws + 2 - 3) / 2 + 1;
+  (void)Hs;
+  return H >= 8 && W >= 8 && (Wq + 6) / 7 <= MAX_TILES;
+}
+
+int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
+                          hipStream_t s) {
+  const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
+  const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
+  const int ntiles = (Wq + 6) / 7;
+  if (ntiles > MAX_TILES || B <= 0) return B <= 0 ? EOSV_OK : (set_error("stem_pool: too wide"), EOSV_ERR_UNSUPPORTED);
+  hipLaunchKernelGGL(stem_pool_bf16_kernel, dim3(B), dim3(64 * ntiles), 0, s, (const u16*)pack, (const u16*)w, bias,
+                     (u16*)y, H, W, Hs, Ws, Hq, Wq);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+}  // namespace eosv
