@@ -288,6 +288,8 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
+  // K = 64 1x1 convs all measured slower than this choice
   if (bf16_variant() == 3 && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
   if (bf16_variant() == 2) {  // 256x256 tiles, 8 waves of 128x64
     if (a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);
