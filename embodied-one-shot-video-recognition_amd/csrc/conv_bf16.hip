@@ -29,7 +29,7 @@ __device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__
 
 // MF = MFMA tile edge: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16; same
 // cycles per FLOP, but the chip holds a higher clock on it with random operands)
-template <int BM, int BN, int WM, int WN, bool STEM, int MF>
+template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BK = 64;  // bf16 elements per row = 128 B
   constexpr int NW = WM * WN;
@@ -40,7 +40,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BI = BN / (8 * NW);
   constexpr int STAGE = (BM + BN) * BK;  // bf16 elements per ring slot
   static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * STAGE];
+  static_assert(NS == 2 || NS == 3, "ring depth");
+  __shared__ __attribute__((aligned(16))) u16 smem[NS * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -145,12 +146,21 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int q = lane / MF;
   const int sw = (r >> 1) & 7;  // tile bases are multiples of 16 rows: the swizzle depends on r only
   const int nk = a.K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // NS-deep ring: NS-1 stages in flight; with NS = 3 the wait before each barrier is a
+  // counted vmcnt (the newest stage stays in flight across it) and barriers are raw
+  // s_barrier (__syncthreads would drain it with vmcnt(0))
+  constexpr int PER = AI + BI;  // DMA instructions per stage per wave
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p);
+  if (NS == 3 && nk > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int cur = 0, wslot = NS - 1;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage((kt + 1) * BK, cur ^ 1);
+    const bool issue = kt + NS - 1 < nk;
+    if (issue) stage((kt + NS - 1) * BK, wslot);
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
     constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
@@ -172,8 +182,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (NS == 3 && issue)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur + 1 == NS ? 0 : cur + 1;
+    wslot = wslot + 1 == NS ? 0 : wslot + 1;
   }
 
   u16* __restrict__ y = (u16*)a.y;
@@ -183,7 +199,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // residual loads and output stores are 16 B (8 bf16) per lane, whole 128-B lines.
   constexpr int EPR = WM * 32;   // rows per pass
   constexpr int EPS = BN + 4;    // f32 row stride
-  static_assert(EPR * EPS * 4 <= 2 * STAGE * 2, "epilogue tile must fit the ring");
+  static_assert(EPR * EPS * 4 <= NS * STAGE * 2, "epilogue tile must fit the ring");
   float* ep = (float*)smem;
   float bcol[TN];
 #pragma unroll
@@ -192,10 +208,38 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
   }
   const int nthreads = 64 * NW;
-  constexpr int TPP = 32 / MF;  // MFMA row-tiles per 32-row pass
+  constexpr int TPP = 32 / MF;                      // MFMA row-tiles per 32-row pass
+  constexpr int NPASS = BM / WM / 32;
+  constexpr int IPT = EPR * (BN / 8) / (64 * NW);   // 16-B output chunks per thread per pass
+  static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
+  // residual chunks of pass i, loaded one pass ahead (pass 0's right after the K-loop) so
+  // their latency overlaps the LDS staging instead of stalling each store
+  uint4 rv[2][IPT];
+  auto chunk = [&](int i, int t, int& lrow, int& c8, long long& o) {
+    const int idx = tid + t * nthreads;
+    lrow = idx / (BN / 8);
+    c8 = idx - lrow * (BN / 8);
+    const int m = m0 + (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
+    const int n = n0 + c8 * 8;
+    o = (m < M && n < a.Cout) ? (long long)m * a.Cout + n : -1;
+  };
+  auto load_res = [&](int i, uint4 (&r4)[IPT]) {
 #pragma unroll
-  for (int i = 0; i < BM / WM / 32; ++i) {
-    __syncthreads();
+    for (int t = 0; t < IPT; ++t) {
+      int lrow, c8;
+      long long o;
+      chunk(i, t, lrow, c8, o);
+      if (o >= 0) r4[t] = *(const uint4*)(res + o);
+    }
+  };
+  if (res) load_res(0, rv[0]);
+#pragma unroll
+  for (int i = 0; i < NPASS; ++i) {
+    if (res && i + 1 < NPASS) load_res(i + 1, rv[(i + 1) & 1]);
+    // raw barriers in the epilogue: only the LDS staging needs ordering, and a
+    // __syncthreads() fence would also wait for the residual prefetch and the stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int t = 0; t < TPP; ++t)
 #pragma unroll
@@ -207,20 +251,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
           const int lrow = wm * 32 + t * MF + crow;
           ep[lrow * EPS + wn * (BN / WN) + j * MF + r] = acc[i * TPP + t][j][e] + bcol[j];
         }
-    __syncthreads();
-    for (int idx = tid; idx < EPR * (BN / 8); idx += nthreads) {
-      const int lrow = idx / (BN / 8);
-      const int c8 = idx - lrow * (BN / 8);
-      const int m = m0 + (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
-      const int n = n0 + c8 * 8;
-      if (m >= M || n >= a.Cout) continue;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int t = 0; t < IPT; ++t) {
+      int lrow, c8;
+      long long o;
+      chunk(i, t, lrow, c8, o);
+      if (o < 0) continue;
       const float4 v0 = *(const float4*)(ep + lrow * EPS + c8 * 8);
       const float4 v1 = *(const float4*)(ep + lrow * EPS + c8 * 8 + 4);
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const long long o = (long long)m * a.Cout + n;
       if (res) {
-        const uint4 rv = *(const uint4*)(res + o);
-        const unsigned ru[4] = {rv.x, rv.y, rv.z, rv.w};
+        const uint4 r4 = rv[i & 1][t];
+        const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff));
@@ -258,15 +302,15 @@ static int bf16_rows() {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, bool STEM>
+template <int BM, int BN, int WM, int WN, bool STEM, int NS = 2>
 static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
   if (bf16_mfma() == 32)
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 32>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 32, NS>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -290,7 +334,10 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
   if (bf16_rows() && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
   // K = 64 1x1 convs all measured slower than this choice
-  if (bf16_variant() == 3 && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
+  const int v = bf16_variant();
+  if (v == 8 && a.Cout == 128) return launch_bf16<256, 128, 4, 2, false, 3>(a, s);  // 144 KiB, 1 block/CU
+  if (v == 9 && a.Cout == 128) return launch_bf16<128, 128, 2, 2, false, 3>(a, s);  // 96 KiB
+  if ((v == 3 || v == 8 || v == 9) && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
   if (bf16_variant() == 2) {  // 256x256 tiles, 8 waves of 128x64
     if (a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);
     if (a.Cout <= 128) return launch_bf16<256, 128, 4, 2, false>(a, s);
