@@ -124,15 +124,49 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     return edist.max_over_ranks(elapsed), torch.cat(preds), prof
 
 
-def roofline(prof, dtype, launches_label=True):
+def measured_traffic(dtype):
+    """HBM bytes per conv launch from the newest profiles/<tag>_traffic.json (written by
+    tools/prof_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    same command); EOSV_TRAFFIC_PROFILE names a specific file.  None if there is none."""
+    import glob
+    path = os.environ.get("EOSV_TRAFFIC_PROFILE") or \
+        (sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))) or [None])[-1]
+    if not path or not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    if dtype not in d:
+        return None, None
+    return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+
+
+def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches):
+    """Conv-family algorithmic bytes per launch: every layer's input + output (+ residual) map
+    once per frame and its weights once per launch (arch.conv_layer_bytes)."""
+    elem = 2 if dtype == "bf16" else 4
+    layers = arch_mod.conv_layer_bytes(arch_mod.SPECS[args.arch], args.res, args.res, elem,
+                                       stem_pool_fused=(dtype == "bf16"))
+    per_frame = sum(b for b, _ in layers)
+    weights = sum(w for _, w in layers)
+    chunks = launches / len(layers)
+    return (frames * per_frame + chunks * weights) / launches
+
+
+def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
     ms, fl, nl = prof
     conv_ms, conv_fl = float(ms.sum()), float(fl.sum())
     achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
     peak = MFMA_PEAK_TF[dtype]
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None,
-            "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
-                      f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
+    out = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(achieved / peak, 4), "traffic": None,
+           "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
+                     f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
+    if args is not None and nl.sum() > 0:
+        tr, src = measured_traffic(dtype)
+        out["traffic"] = tr
+        out["traffic_unit"] = "HBM bytes per conv launch"
+        out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, int(nl.sum())))
+        out["traffic_source"] = src
+    return out
 
 
 def main():
@@ -162,7 +196,8 @@ def main():
 
     elapsed, pred, prof = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
     clips = edist.sum_over_ranks(sum(d.batch.n_clips for d in batches[args.warmup:]))
-    frames = edist.sum_over_ranks(sum(d.batch.n_frames for d in batches[args.warmup:]))
+    frames_rank = sum(d.batch.n_frames for d in batches[args.warmup:])
+    frames = edist.sum_over_ranks(frames_rank)
     # (episode, prediction) pairs: ONE all-gather over xGMI (RCCL) after the timed region
     preds = edist.gather_predictions(timed_idx, pred.cpu().numpy(), len(plans))
     timed = preds >= 0
@@ -177,12 +212,12 @@ def main():
                      "ms_per_step": round(el2 / args.steps * 1e3, 3),
                      "prediction_agreement_vs_primary": round(float((preds2[timed] == preds[timed]).mean()), 4),
                      "episode_acc": round(float((preds2[timed] == qy[timed]).mean()), 4),
-                     "roofline": roofline(prof2, args.secondary_dtype)}
+                     "roofline": roofline(prof2, args.secondary_dtype, args, arch_mod, frames_rank)}
 
     if rank == 0:
         ms, fl, nl = prof
         gflop_frame = 2 * arch_mod.conv_macs_per_frame(arch_mod.SPECS[args.arch], args.res, args.res) / 1e9
-        rl = roofline(prof, args.dtype)
+        rl = roofline(prof, args.dtype, args, arch_mod, frames_rank)
         rl["end_to_end_tflops"] = round(frames * gflop_frame / elapsed / 1e3, 2)
         rl["flop_per_frame"] = round(gflop_frame * 1e9)
         out = {

@@ -44,7 +44,20 @@ struct ConvArgs {
   int relu;
   const void* zero;   // >= 64 zeroed bytes (DMA target for out-of-bounds taps)
   int abl;            // ablation bits for profiling builds (0 = normal)
+  int xcd;            // 1: XCD-aware block order (each XCD walks a contiguous range of tiles)
+  int kcm;            // bf16 only: K ordered (cin/64, kh, kw, cin%64) instead of (kh, kw, cin)
 };
+
+// Workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one L2;
+// MI355X_MICROARCH.md, Workgroup dispatch).  Remap so that XCD x processes the contiguous
+// logical tiles [x*q + min(x, r), ...): neighbouring M-tiles (which share input halo rows)
+// and the N-tiles of one M-tile (which share the A rows) then hit the same L2.  Bijective
+// on [0, nb) for any nb; placement is a speed hint only, never a correctness assumption.
+__device__ __forceinline__ int xcd_tile(int b, int nb, int on) {
+  if (!on) return b;
+  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return x * q + (x < r ? x : r) + i;
+}
 
 int launch_conv_f32(const ConvArgs& a, hipStream_t s);
 int launch_conv_f32_dma(const ConvArgs& a, hipStream_t s, int variant);
@@ -52,6 +65,9 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 bool stem_pool_bf16_ok(int H, int W);  // stem_pool_bf16.hip: fused stem conv + ReLU + maxpool
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                           hipStream_t s);
+bool conv_bf16_p8_ok(const ConvArgs& a);  // conv_bf16_p8.hip: phased 8-wave implicit GEMM
+bool conv_bf16_p8_default(const ConvArgs& a);
+int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 

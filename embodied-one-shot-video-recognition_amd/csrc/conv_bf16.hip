@@ -50,8 +50,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int HoWo = a.Ho * a.Wo;
   const int M = a.N * HoWo;
   const int nN = (a.Cout + BN - 1) / BN;
-  const int mt = blockIdx.x / nN;
-  const int nt = blockIdx.x - mt * nN;
+  const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
+  const int mt = bt / nN;
+  const int nt = bt - mt * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const u16* __restrict__ x = (const u16*)a.x;
   const u16* __restrict__ w = (const u16*)a.w;
@@ -96,10 +97,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 8 : nullptr;
   }
 
-  auto stage = [&](int k0, int slot) {
+  auto stage = [&](int k0, int slot, int skip) {
     u16* As = smem + slot * STAGE;
     u16* Bs = As + BM * BK;
-    if constexpr (STEM) {
+    if (skip & 4) {
+    } else if constexpr (STEM) {
 #pragma unroll
       for (int j = 0; j < AI; ++j) {
         const int g = (k0 >> 3) + alc[j];
@@ -110,8 +112,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     } else {
-      const int tap = k0 / a.Cin;
-      const int c0 = k0 - tap * a.Cin;
+      int tap, c0;
+      if (a.kcm) {  // K = (cin / 64, kh, kw, cin % 64)
+        const int taps = a.KH * a.KW;
+        const int chunk = k0 / (64 * taps);
+        tap = (k0 - chunk * 64 * taps) >> 6;
+        c0 = chunk * 64;
+      } else {
+        tap = k0 / a.Cin;
+        c0 = k0 - tap * a.Cin;
+      }
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
       const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;
@@ -124,6 +134,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     }
+    if (skip & 8) return;
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
       const u16* src = brow[j] ? brow[j] + k0 : zero;
@@ -150,7 +161,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // counted vmcnt (the newest stage stays in flight across it) and barriers are raw
   // s_barrier (__syncthreads would drain it with vmcnt(0))
   constexpr int PER = AI + BI;  // DMA instructions per stage per wave
-  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p);
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p, 0);
   if (NS == 3 && nk > 1)
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
   else
@@ -160,7 +171,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   int cur = 0, wslot = NS - 1;
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
-    if (issue) stage((kt + NS - 1) * BK, wslot);
+    // a.abl (profiling-only ablations, results wrong when set): 1 no main-loop loads,
+    // 4 no A loads, 8 no B loads, 2 no output stores
+    if (issue && !(a.abl & 1)) stage((kt + NS - 1) * BK, wslot, a.abl);
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
     constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
@@ -281,7 +294,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         }
         pk[k] = (unsigned)f_to_bf(lo) | ((unsigned)f_to_bf(hi) << 16);
       }
-      *(uint4*)(y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      if (a.abl & 2)
+        asm volatile("" ::"v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]));
+      else
+        *(uint4*)(y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     }
   }
 }
@@ -315,6 +331,14 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   return EOSV_OK;
 }
 
+static int bf16_p8() {
+  static int v = [] {
+    const char* e = getenv("EOSV_BF16_P8");  // 0 never, 1 default shapes, 2 every eligible shape (A/B switch)
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static int bf16_variant() {
   static int v = [] {
     const char* e = getenv("EOSV_BF16_TILE");
@@ -323,7 +347,13 @@ static int bf16_variant() {
   return v;
 }
 
-int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
+int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
+  static const int abl = [] {
+    const char* e = getenv("EOSV_CONV_ABL");  // profiling-only ablations; results are wrong when set
+    return e ? atoi(e) : 0;
+  }();
+  ConvArgs a = a0;
+  a.abl = abl;
   const bool stem = (a.Cin == 3);
   if (!a.zero || a.K % 64 != 0 || (!stem && a.Cin % 64 != 0) ||
       (stem && (a.KWp != 8 || a.KW != 7 || a.stride % 2 != 0 || a.K != (a.KH * 24 + 63) / 64 * 64))) {
@@ -332,6 +362,7 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  if (bf16_p8() && conv_bf16_p8_ok(a) && (bf16_p8() == 2 || conv_bf16_p8_default(a))) return launch_conv_bf16_p8(a, s);
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
   // K = 64 1x1 convs all measured slower than this choice
   const int v = bf16_variant();

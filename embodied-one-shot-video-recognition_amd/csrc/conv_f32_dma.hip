@@ -52,8 +52,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   const int HoWo = a.Ho * a.Wo;
   const int M = a.N * HoWo;
   const int nN = (a.Cout + BN - 1) / BN;
-  const int mt = blockIdx.x / nN;
-  const int nt = blockIdx.x - mt * nN;
+  const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
+  const int mt = bt / nN;
+  const int nt = bt - mt * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const float* __restrict__ x = (const float*)a.x;
   const float* __restrict__ w = (const float*)a.w;

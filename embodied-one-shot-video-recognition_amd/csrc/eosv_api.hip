@@ -24,6 +24,7 @@ void set_error(const std::string& msg) { g_err = msg; }
 struct Conv {
   int cin = 0, cout = 0, kh = 1, kw = 1, kwp = 1, cinp = 0, stride = 1, pad = 0, K = 0;
   bool stem = false;
+  bool kcm = false;           // bf16 weights in chunk-major K order (ConvArgs::kcm)
   int id = 0;                 // layer id for profiling (plan order)
   std::string wname, bnname;  // state_dict prefixes
   void* w = nullptr;          // [cout][K] (f32 or bf16)
@@ -233,13 +234,19 @@ static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, boo
     if (!bias) return EOSV_ERR_ARG;
     for (int o = 0; o < c.cout; ++o) beta[o] = bias[o];
   }
+  // bf16 multi-tap convs with Cin > 64: K chunk-major, (cin / 64, kh, kw, cin % 64), so that a
+  // conv's K walk visits all taps of one 64-channel slice of the input before the next slice
+  // and the block's input patch is re-read from L2, not from beyond it (conv_bf16_p8.hip)
+  c.kcm = bf16 && !c.stem && c.cinp % 64 == 0 && c.cinp > 64 && c.kh * c.kw > 1 && c.kwp == c.kw;
   std::vector<float> wf((size_t)c.cout * c.K, 0.f);
   for (int o = 0; o < c.cout; ++o)
     for (int i = 0; i < c.cin; ++i)
       for (int y = 0; y < c.kh; ++y)
         for (int x = 0; x < c.kw; ++x) {
           const float v = w[(((size_t)o * c.cin + i) * c.kh + y) * c.kw + x];
-          wf[(size_t)o * c.K + ((size_t)y * c.kwp + x) * c.cinp + i] = v * alpha[o];
+          const size_t k = c.kcm ? ((size_t)(i / 64) * c.kh * c.kw + y * c.kw + x) * 64 + i % 64
+                                 : ((size_t)y * c.kwp + x) * c.cinp + i;
+          wf[(size_t)o * c.K + k] = v * alpha[o];
         }
   int rc;
   if (bf16) {
@@ -288,6 +295,12 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   a.K = c.K;
   a.relu = relu ? 1 : 0;
   a.zero = h->zero;
+  static const int xcd = [] {
+    const char* e = getenv("EOSV_XCD");  // 0 = plain blockIdx order (A/B switch)
+    return e ? atoi(e) : 1;
+  }();
+  a.xcd = xcd;
+  a.kcm = c.kcm ? 1 : 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);

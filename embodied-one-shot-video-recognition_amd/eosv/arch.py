@@ -108,3 +108,39 @@ def conv_macs_per_frame(spec: ResNetSpec, H: int = 224, W: int = 224) -> int:
             h, w = ho, wo
             inplanes = cout
     return macs
+
+
+def conv_layer_bytes(spec: ResNetSpec, H: int = 224, W: int = 224, elem: int = 4, stem_pool_fused: bool = False):
+    """Algorithmic HBM bytes of every conv launch, in the native plan's layer-id order
+    (stem, then per block c1, c2[, c3][, downsample]: csrc/eosv_api.hip): a list of
+    (per-frame bytes, per-launch weight bytes).  Per frame: the input map read once, the
+    output map written once, plus the residual map read once by the block's last conv.
+    The stem reads the 3-channel frame; with ``stem_pool_fused`` (bf16 path) it writes the
+    pooled map.  This is the floor the rocprofv3 FETCH/WRITE traffic is compared with."""
+    def out_hw(h, k, s, p):
+        return (h + 2 * p - k) // s + 1
+
+    layers = []
+    h, w = out_hw(H, 7, 2, 3), out_hw(W, 7, 2, 3)
+    ph, pw = out_hw(h, 3, 2, 1), out_hw(w, 3, 2, 1)
+    out = (ph * pw if stem_pool_fused else h * w) * 64
+    layers.append(((3 * H * W + out) * elem, 64 * 147 * elem))
+    h, w = ph, pw
+    inplanes = 64
+    for li, (planes, n) in enumerate(zip((64, 128, 256, 512), spec.layers)):
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            cout = planes * spec.expansion
+            ho, wo = out_hw(h, 3, s, 1), out_hw(w, 3, s, 1)
+            if spec.block == "basic":
+                layers.append(((h * w * inplanes + ho * wo * planes) * elem, planes * inplanes * 9 * elem))
+                layers.append(((2 * ho * wo * planes + ho * wo * cout) * elem, cout * planes * 9 * elem))
+            else:
+                layers.append(((h * w * inplanes + h * w * planes) * elem, planes * inplanes * elem))
+                layers.append(((h * w * planes + ho * wo * planes) * elem, planes * planes * 9 * elem))
+                layers.append(((ho * wo * planes + 2 * ho * wo * cout) * elem, cout * planes * elem))
+            if bi == 0 and (s != 1 or inplanes != cout):
+                layers.append(((ho * wo * inplanes + ho * wo * cout) * elem, cout * inplanes * elem))
+            h, w = ho, wo
+            inplanes = cout
+    return layers

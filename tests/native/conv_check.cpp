@@ -86,13 +86,16 @@ static float bf2f(unsigned short v) {
   return f;
 }
 
-// bf16 3x3/s1/p1 conv through launch_conv_bf16 (stage-1 shapes take the row-strip kernel);
-// reference in double on the bf16-rounded operands, checked on images `checked` only
-static int check_bf16(int N, int H, int W, int C, bool res, bool relu) {
-  const int K = 9 * C;
+// bf16 conv through launch_conv_bf16 (stage-1 3x3 shapes take the row-strip kernel, Cout >= 128
+// the phased 8-wave kernel); reference in double on the bf16-rounded operands, checked on images
+// `checked` only
+static int check_bf16(int N, int H, int W, int Cin, int Cout, int k, int stride, int pad, bool res, bool relu,
+                      bool kcm = false) {
+  const int K = k * k * Cin;
+  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
   unsigned s = 777;
-  std::vector<unsigned short> x((size_t)N * H * W * C), w((size_t)C * K), r((size_t)N * H * W * C);
-  std::vector<float> b(C);
+  std::vector<unsigned short> x((size_t)N * H * W * Cin), w((size_t)Cout * K), r((size_t)N * Ho * Wo * Cout);
+  std::vector<float> b(Cout);
   for (auto& v : x) v = f2bf(frand(s));
   for (auto& v : w) v = f2bf(frand(s) * 0.1f);
   for (auto& v : r) v = f2bf(frand(s));
@@ -101,50 +104,61 @@ static int check_bf16(int N, int H, int W, int C, bool res, bool relu) {
   float* db;
   void* dz;
   hipMalloc(&dx, x.size() * 2); hipMalloc(&dw, w.size() * 2); hipMalloc(&dr, r.size() * 2);
-  hipMalloc(&dy, r.size() * 2); hipMalloc(&db, C * 4); hipMalloc(&dz, 256); hipMemset(dz, 0, 256);
+  hipMalloc(&dy, r.size() * 2); hipMalloc(&db, Cout * 4); hipMalloc(&dz, 256); hipMemset(dz, 0, 256);
   hipMemcpy(dx, x.data(), x.size() * 2, hipMemcpyHostToDevice);
-  hipMemcpy(dw, w.data(), w.size() * 2, hipMemcpyHostToDevice);
+  {
+    // kcm: device weights in K order (cin / 64, kh, kw, cin % 64) (ConvArgs::kcm)
+    std::vector<unsigned short> wd(w.size());
+    for (int o = 0; o < Cout; ++o)
+      for (int t = 0; t < k * k; ++t)
+        for (int c = 0; c < Cin; ++c)
+          wd[(size_t)o * K + (kcm ? ((c / 64) * k * k + t) * 64 + c % 64 : t * Cin + c)] = w[(size_t)o * K + t * Cin + c];
+    hipMemcpy(dw, wd.data(), wd.size() * 2, hipMemcpyHostToDevice);
+  }
   hipMemcpy(dr, r.data(), r.size() * 2, hipMemcpyHostToDevice);
-  hipMemcpy(db, b.data(), C * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db, b.data(), Cout * 4, hipMemcpyHostToDevice);
   hipMemset(dy, 0xff, r.size() * 2);
   ConvArgs a{};
   a.x = dx; a.w = dw; a.bias = db; a.res = res ? dr : nullptr; a.y = dy;
-  a.N = N; a.H = H; a.W = W; a.Cin = C; a.Ho = H; a.Wo = W; a.Cout = C;
-  a.KH = 3; a.KW = 3; a.KWp = 3; a.stride = 1; a.pad = 1; a.K = K; a.relu = relu; a.zero = dz;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.KH = k; a.KW = k; a.KWp = k; a.stride = stride; a.pad = pad; a.K = K; a.relu = relu; a.zero = dz;
+  a.xcd = 1;
+  a.kcm = kcm;
   const int rc = launch_conv_bf16(a, 0);
   hipDeviceSynchronize();
   std::vector<unsigned short> y(r.size());
   hipMemcpy(y.data(), dy, y.size() * 2, hipMemcpyDeviceToHost);
-  const int checked[4] = {0, 1, N - 2, N - 1};
+  const int checked[4] = {0, N > 1 ? 1 : 0, N > 2 ? N - 2 : 0, N - 1};
   double maxerr = 0;
   long bad = 0;
   for (int ci = 0; ci < 4; ++ci) {
     const int n = checked[ci];
-    for (int oh = 0; oh < H; ++oh)
-      for (int ow = 0; ow < W; ++ow)
-        for (int o = 0; o < C; ++o) {
+    if (ci > 0 && n == checked[ci - 1]) continue;
+    for (int oh = 0; oh < Ho; ++oh)
+      for (int ow = 0; ow < Wo; ++ow)
+        for (int o = 0; o < Cout; ++o) {
           double acc = b[o];
-          for (int kh = 0; kh < 3; ++kh)
-            for (int kw = 0; kw < 3; ++kw) {
-              const int ih = oh - 1 + kh, iw = ow - 1 + kw;
+          for (int kh = 0; kh < k; ++kh)
+            for (int kw = 0; kw < k; ++kw) {
+              const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
               if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-              for (int c = 0; c < C; ++c)
-                acc += (double)bf2f(x[(((size_t)n * H + ih) * W + iw) * C + c]) *
-                       bf2f(w[(size_t)o * K + (kh * 3 + kw) * C + c]);
+              for (int c = 0; c < Cin; ++c)
+                acc += (double)bf2f(x[(((size_t)n * H + ih) * W + iw) * Cin + c]) *
+                       bf2f(w[(size_t)o * K + (kh * k + kw) * Cin + c]);
             }
-          const size_t oi = (((size_t)n * H + oh) * W + ow) * C + o;
+          const size_t oi = (((size_t)n * Ho + oh) * Wo + ow) * Cout + o;
           if (res) acc += bf2f(r[oi]);
           if (relu && acc < 0) acc = 0;
           const double e = fabs(acc - bf2f(y[oi]));
-          if (e > 1e-2 * (1 + fabs(acc))) {
+          if (!(e <= 1e-2 * (1 + fabs(acc)))) {
             if (bad < 5) printf("  bad n%d oh%d ow%d o%d ref %f got %f\n", n, oh, ow, o, acc, bf2f(y[oi]));
             ++bad;
           }
           maxerr = fmax(maxerr, e);
         }
   }
-  printf("%s bf16 N%d H%d W%d C%d res%d relu%d rc=%d maxerr %.3e bad %ld\n", bad ? "FAIL" : "ok  ", N, H, W, C, res,
-         relu, rc, maxerr, bad);
+  printf("%s bf16 N%d H%d W%d Cin%d Cout%d k%d s%d p%d res%d relu%d kcm%d rc=%d maxerr %.3e bad %ld\n",
+         bad ? "FAIL" : "ok  ", N, H, W, Cin, Cout, k, stride, pad, res, relu, kcm, rc, maxerr, bad);
   hipFree(dx); hipFree(dw); hipFree(dr); hipFree(dy); hipFree(db); hipFree(dz);
   return bad || rc ? 1 : 0;
 }
@@ -223,8 +237,24 @@ int main() {
   fails += check_stem_pool(3, 100, 86);  // ragged: partial last column tile, odd pooled sizes
   fails += check_stem_pool(2, 64, 48);
   // stage-1 shape (row-strip kernel): 300 images = 4200 strips, several strips per workgroup
-  fails += check_bf16(300, 56, 56, 64, true, true);
-  fails += check_bf16(3, 56, 56, 64, false, true);
+  fails += check_bf16(300, 56, 56, 64, 64, 3, 1, 1, true, true);
+  fails += check_bf16(3, 56, 56, 64, 64, 3, 1, 1, false, true);
+  // phased 8-wave kernel: 512x128 (Cout 128) and 256x256 tiles, strided entries, 1x1s, M tails
+  fails += check_bf16(40, 28, 28, 128, 128, 3, 1, 1, true, true);
+  fails += check_bf16(40, 28, 28, 128, 128, 3, 1, 1, true, true, true);
+  fails += check_bf16(30, 14, 14, 256, 256, 3, 1, 1, true, true, true);
+  fails += check_bf16(9, 28, 28, 128, 256, 3, 2, 1, false, true, true);
+  fails += check_bf16(3, 7, 7, 512, 512, 3, 1, 1, false, true, true);
+  fails += check_bf16(2, 9, 11, 128, 128, 3, 1, 1, true, false, true);
+  fails += check_bf16(7, 56, 56, 64, 128, 3, 2, 1, false, true);
+  fails += check_bf16(7, 56, 56, 64, 128, 1, 2, 0, false, false);
+  fails += check_bf16(30, 14, 14, 256, 256, 3, 1, 1, true, true);
+  fails += check_bf16(9, 28, 28, 128, 256, 3, 2, 1, false, true);
+  fails += check_bf16(20, 7, 7, 512, 512, 3, 1, 1, true, true);
+  fails += check_bf16(3, 7, 7, 512, 512, 3, 1, 1, false, true);  // M = 147 < one 256-row tile
+  fails += check_bf16(5, 14, 14, 1024, 256, 1, 1, 0, false, true);
+  fails += check_bf16(5, 14, 14, 256, 1024, 1, 1, 0, true, true);
+  fails += check_bf16(2, 9, 11, 128, 128, 3, 1, 1, true, false);  // ragged map, M = 198
   fails += check(1, 8, 8, 32, 64, 1, 1, 0, false, false, false);
   fails += check(2, 9, 7, 64, 64, 3, 1, 1, false, false, false);
   fails += check(2, 14, 14, 64, 128, 3, 2, 1, false, true, true);
