@@ -205,7 +205,8 @@ __global__ __launch_bounds__(256) void seg_dist_kernel(const float* __restrict__
   }
 }
 
-// smoothed[s][g] = l1*d[s-1][g] + l2*d[s][g] + l1*d[s+1][g] (zero padded), argmin over g
+// smoothed[s][g] = l1*d[s-1][g] + l2*d[s][g] + l1*d[s+1][g] (zero padded at the ends of each
+// episode's S rows), argmin over g; one block per row of the n_episodes*S rows
 __global__ __launch_bounds__(256) void seg_smooth_argmin_kernel(const float* __restrict__ dist, int S,
                                                                 int G, float l1, float l2,
                                                                 long long* __restrict__ ids,
@@ -213,12 +214,13 @@ __global__ __launch_bounds__(256) void seg_smooth_argmin_kernel(const float* __r
   __shared__ float bvs[4];
   __shared__ int bis[4];
   const int s = blockIdx.x;
+  const int sl = s % S;  // row within its episode
   float bv = INFINITY;
   int bi = 0x7fffffff;
   for (int g = threadIdx.x; g < G; g += 256) {
-    const float dm = s > 0 ? dist[(long long)(s - 1) * G + g] : 0.f;
+    const float dm = sl > 0 ? dist[(long long)(s - 1) * G + g] : 0.f;
     const float d0 = dist[(long long)s * G + g];
-    const float dp = s + 1 < S ? dist[(long long)(s + 1) * G + g] : 0.f;
+    const float dp = sl + 1 < S ? dist[(long long)(s + 1) * G + g] : 0.f;
     const float v = fmaf(l1, dp, fmaf(l2, d0, l1 * dm));
     if (out) out[(long long)s * G + g] = v;
     if (v < bv) {  // g increases per thread, so '<' keeps the first minimum
@@ -309,19 +311,21 @@ extern "C" int eosv_match(const float* d_query, const float* d_support, const in
   return EOSV_OK;
 }
 
-extern "C" int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G, int D,
-                                  float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
-                                  eosv_stream_t stream) {
-  if (S <= 0 || G <= 0 || D <= 0 || !d_seg || !d_gallery || !d_ids) {
+extern "C" int eosv_segment_match_episodes(const float* d_seg, int n_episodes, int S, const float* d_gallery,
+                                           int G, int D, float lamda1, float lamda2, int64_t* d_ids,
+                                           float* d_dist, eosv_stream_t stream) {
+  if (n_episodes <= 0 || S <= 0 || G <= 0 || D <= 0 || !d_seg || !d_gallery || !d_ids ||
+      (long long)n_episodes * S > 0x7fffffffLL) {
     set_error("eosv_segment_match: bad argument");
     return EOSV_ERR_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
+  const int R = n_episodes * S;  // all episodes' rows against the one gallery: a grid that fills the chip
   float* raw = nullptr;
-  EOSV_HIP_CHECK(hipMallocAsync((void**)&raw, sizeof(float) * (size_t)S * G, s));
-  dim3 grid((G + SG_G - 1) / SG_G, (S + SG_S - 1) / SG_S);
-  hipLaunchKernelGGL(seg_dist_kernel, grid, dim3(256), 0, s, d_seg, S, d_gallery, G, D, raw);
-  hipLaunchKernelGGL(seg_smooth_argmin_kernel, dim3(S), dim3(256), 0, s, raw, S, G, lamda1, lamda2,
+  EOSV_HIP_CHECK(hipMallocAsync((void**)&raw, sizeof(float) * (size_t)R * G, s));
+  dim3 grid((G + SG_G - 1) / SG_G, (R + SG_S - 1) / SG_S);
+  hipLaunchKernelGGL(seg_dist_kernel, grid, dim3(256), 0, s, d_seg, R, d_gallery, G, D, raw);
+  hipLaunchKernelGGL(seg_smooth_argmin_kernel, dim3(R), dim3(256), 0, s, raw, S, G, lamda1, lamda2,
                      (long long*)d_ids, d_dist);
   const hipError_t le = hipGetLastError();
   EOSV_HIP_CHECK(hipFreeAsync(raw, s));
@@ -330,4 +334,10 @@ extern "C" int eosv_segment_match(const float* d_seg, int S, const float* d_gall
     return EOSV_ERR_HIP;
   }
   return EOSV_OK;
+}
+
+extern "C" int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G, int D,
+                                  float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
+                                  eosv_stream_t stream) {
+  return eosv_segment_match_episodes(d_seg, 1, S, d_gallery, G, D, lamda1, lamda2, d_ids, d_dist, stream);
 }

@@ -187,6 +187,25 @@ def segment_match(seg: torch.Tensor, gallery: torch.Tensor, lamda1: float, lamda
     return ids, dist
 
 
+def segment_match_episodes(seg: torch.Tensor, n_episodes: int, gallery: torch.Tensor, lamda1: float,
+                           lamda2: float, with_dist: bool = False, stream=None):
+    """segment_match for n_episodes independent episodes in one call: seg [n_episodes*S, D]
+    episode-major -> ids [n_episodes*S] (smoothing never crosses an episode boundary)."""
+    _require_cuda(seg, "seg", torch.float32)
+    _require_cuda(gallery, "gallery", torch.float32)
+    R, D = seg.shape
+    if n_episodes <= 0 or R % n_episodes:
+        raise ValueError("seg rows must be a multiple of n_episodes")
+    G = gallery.shape[0]
+    ids = torch.empty(R, device=seg.device, dtype=torch.int64)
+    dist = torch.empty(R, G, device=seg.device, dtype=torch.float32) if with_dist else None
+    check(lib().eosv_segment_match_episodes(ptr(seg), n_episodes, R // n_episodes, ptr(gallery), G, D,
+                                            float(lamda1), float(lamda2), ptr(ids),
+                                            ptr(dist) if dist is not None else None, stream_ptr(stream)),
+          "eosv_segment_match_episodes")
+    return ids, dist
+
+
 def temporal_smooth(x: torch.Tensor, lamda1: float, lamda2: float, stream=None) -> torch.Tensor:
     """3-tap [l1,l2,l1] smoothing along the last axis, zero padded (models.py:42-56)."""
     _require_cuda(x, "x", torch.float32)

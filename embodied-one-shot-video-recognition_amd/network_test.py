@@ -21,6 +21,8 @@ frame directories are decoded on the host (eosv.frames).
 import copy
 import warnings
 
+import os
+
 import numpy as np
 import torch
 
@@ -226,13 +228,20 @@ class TestNetwork():
 
     # ------------------------------------------------------------------ config 3
     def gallery_features(self):
-        """Gallery segment features [G*T/seg_len, D] on the device (network_test.py:184-189)."""
+        """Gallery segment features [G*T/seg_len, D] on the device (network_test.py:184-189).
+
+        Also keeps the raw (pre-L2) per-frame gallery features, np.resize'd like the segment
+        features: the augmented videos of aug_seg_T are assembled from gallery and support
+        FRAMES, and the backbone is a per-frame 2D CNN whose kernels compute every frame with
+        the same instruction sequence wherever it sits in a batch, so their features are
+        gathered instead of re-running the backbone on the assembled frames (bit-identical;
+        EOSV_AUG_REFORWARD=1 re-runs it, as the reference does at network_test.py:210-248)."""
         H, W = utils.IMG_crop_size
         T, sl = utils.VIDEO_FRAMES, utils.seg_len
         dev = torch.device('cuda', torch.cuda.current_device())
         infos = _gad.gallery_video_infos()
-        feats = []
-        self._gallery_frames = []
+        feats, raws = [], []
+        self._gallery_frames = [] if self._aug_reforward() else None
         for g0 in range(0, len(infos), 64):
             clips = []
             for vi in infos[g0:g0 + 64]:
@@ -242,14 +251,17 @@ class TestNetwork():
                                      "(the reference's torch.stack fails on it too)")
                 clips.append((vi, ids, T))
             fr = self._clip_frames(clips, H, W, dev)
-            self._gallery_frames.append(fr)
+            if self._gallery_frames is not None:
+                self._gallery_frames.append(fr)
             f = self._features(fr)
+            raws.append(f)
             if self.L2:
                 n = f.shape[0]
                 f = _engine.clip_embed(f, torch.arange(n, dtype=torch.int32, device=dev),
                                        torch.ones(n, dtype=torch.int32, device=dev), True)
             feats.append(f)
         feat = torch.cat(feats)
+        raw = torch.cat(raws)
         if feat.shape[1] != 2048:
             raise ValueError("test_network_aug_segment needs a 2048-d backbone (resnet50/101): the reference "
                              "np.resize's features to 2048 (network_test.py:188,204)")
@@ -257,8 +269,15 @@ class TestNetwork():
         if feat.shape[0] != n_seg * sl:  # np.resize semantics: repeat/truncate the flat array
             reps = torch.arange(n_seg * sl, device=dev) % feat.shape[0]
             feat = feat[reps].contiguous()
-        self._gallery_frames = torch.cat(self._gallery_frames)
+            raw = raw[reps].contiguous()
+        self._gallery_raw = raw
+        if self._gallery_frames is not None:
+            self._gallery_frames = torch.cat(self._gallery_frames)
         return _engine.segment_mean(feat, sl)
+
+    @staticmethod
+    def _aug_reforward():
+        return os.environ.get("EOSV_AUG_REFORWARD", "0") == "1"
 
     def test_network_aug_segment(self, pre_model=None, data_aug='aug_seg_T'):
         """network_test.py:170-267, batched on the device."""
@@ -309,11 +328,9 @@ class TestNetwork():
                                     torch.ones(n_sup_frames, dtype=torch.int32, device=dev), True)
         seg = _engine.segment_mean(sf.contiguous(), sl)  # [E*nk*ns_v, D]
         S = nk * ns_v
-        pool = []
-        for e in range(E):
-            ids, _ = _engine.segment_match(seg[e * S:(e + 1) * S].contiguous(), gal, utils.lamda1, utils.lamda2)
-            pool.append(ids)
-        pool = torch.stack(pool).view(E, nk, ns_v)  # np.resize(pool_ids, (n*k, num_segs))
+        # every episode's segments against the gallery in one launch (per-episode smoothing)
+        pool, _ = _engine.segment_match_episodes(seg.contiguous(), E, gal, utils.lamda1, utils.lamda2)
+        pool = pool.view(E, nk, ns_v)  # np.resize(pool_ids, (n*k, num_segs))
         # augmented videos: support video i with segment s <- gallery segment pool[e,i,s]
         f = torch.arange(T, device=dev)
         seg_of = f // sl
@@ -321,11 +338,13 @@ class TestNetwork():
         sup_rows = (torch.arange(E * nk, device=dev).view(E, nk, 1, 1) * T + f.view(1, 1, 1, T))
         gal_rows = (pool.view(E, nk, ns_v, 1) * sl + (f % sl).view(1, 1, 1, T))
         use_gal = (seg_of.view(1, 1, 1, T) == s_idx.view(1, 1, ns_v, 1))
-        n_gal = self._gallery_frames.shape[0]
+        n_gal = self._gallery_raw.shape[0]
         rows = torch.where(use_gal, gal_rows, n_gal + sup_rows.expand(E, nk, ns_v, T)).reshape(-1)
-        src = torch.cat([self._gallery_frames, frames[:n_sup_frames]])
-        aug_frames = src.index_select(0, rows)
-        aug_feat = self._features(aug_frames)
+        if self._gallery_frames is not None:  # the reference's way: forward the assembled frames
+            src = torch.cat([self._gallery_frames, frames[:n_sup_frames]])
+            aug_feat = self._features(src.index_select(0, rows))
+        else:  # per-frame CNN: gather the frames' features (see gallery_features)
+            aug_feat = torch.cat([self._gallery_raw, feat[:n_sup_frames]]).index_select(0, rows).contiguous()
         n_aug = E * nk * ns_v
         aug_emb = _engine.clip_embed(aug_feat, torch.arange(n_aug, dtype=torch.int32, device=dev) * T,
                                      torch.full((n_aug,), T, dtype=torch.int32, device=dev), bool(self.L2))

@@ -107,6 +107,13 @@ int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G,
                        float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
                        eosv_stream_t stream);
 
+/* The same for n_episodes independent episodes in one call (network_test.py:207-214 run per
+ * episode): d_seg [n_episodes*S, D] (episode-major), one shared gallery; the smoothing never
+ * crosses an episode boundary.  d_ids [n_episodes*S]; d_dist [n_episodes*S, G] or NULL. */
+int eosv_segment_match_episodes(const float* d_seg, int n_episodes, int S, const float* d_gallery, int G,
+                                int D, float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
+                                eosv_stream_t stream);
+
 /* TemporalLayer (models.py:42-56, PyTorch-1.x conv semantics): y[r][c] = l1*x[r][c-1]
  * + l2*x[r][c] + l1*x[r][c+1] along the last axis, zero padded; d_x/d_y [rows, cols]. */
 int eosv_temporal_smooth(const float* d_x, int rows, int cols, float lamda1, float lamda2,

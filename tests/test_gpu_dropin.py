@@ -115,12 +115,12 @@ def test_temporal_layer_dropin():
     assert y.shape == (1, 1, 5120, 40)
 
 
-def test_aug_segment_reproduces_reference(tmp_path):
-    """Config-3 path (R50, aug_seg_T) against the reference's own run (2 episodes)."""
+def _run_c3(tmp_path, reforward, monkeypatch):
     import generate_augmented_datasets as gad
     import network_test
     import utils
 
+    monkeypatch.setenv("EOSV_AUG_REFORWARD", reforward)
     meta, arr = load_fixture("c3_r50_aug_seed4")
     pkl = str(tmp_path / "model.pkl")
     _save_sd("resnet50", pkl)
@@ -132,14 +132,19 @@ def test_aug_segment_reproduces_reference(tmp_path):
         np.random.seed(meta["seed"])
         gad.generate_gallery_list()
         assert gad.gallery_video_infos() == meta["gallery"]
-        acc_path = str(tmp_path / "acc.txt")
+        acc_path = str(tmp_path / f"acc{reforward}.txt")
         tn = network_test.TestNetwork(acc_path, "resnet50", "protonet", True)
         tn.debug = {}
         tn.test_network_aug_segment(pre_model=pkl)
         tn.acc_file.close()
     finally:
         utils.GALLERY_LIST, utils.EPISODE_NUMS["test"] = old
-    dbg = tn.debug
+    return tn.debug, open(acc_path).read(), meta, arr
+
+
+def test_aug_segment_reproduces_reference(tmp_path, monkeypatch):
+    """Config-3 path (R50, aug_seg_T) against the reference's own run (2 episodes)."""
+    dbg, acc_text, meta, arr = _run_c3(tmp_path, "0", monkeypatch)
     ref_pool = np.argsort(arr["smoothed"], axis=2)[:, :, 0]  # [E,40] (network_test.py:211-212)
     got_pool = dbg["pool"].cpu().numpy().reshape(len(meta["episodes"]), -1)
     assert np.array_equal(got_pool, ref_pool)
@@ -149,4 +154,14 @@ def test_aug_segment_reproduces_reference(tmp_path):
     q = dbg["q_emb"].cpu().numpy()
     assert np.abs(q - arr["query_feature"][:, 0]).max() / np.abs(arr["query_feature"]).max() < 1e-4
     assert np.array_equal(dbg["pred"].cpu().numpy(), arr["pred"][:, 0])
-    assert open(acc_path).read() == meta["acc_file"]
+    assert acc_text == meta["acc_file"]
+
+
+def test_aug_segment_feature_gather_equals_reforward(tmp_path, monkeypatch):
+    """The augmented videos' features gathered from the gallery / support frame features are
+    bit-identical to re-running the backbone on the assembled frames (the reference's way)."""
+    a, acc_a, _, _ = _run_c3(tmp_path, "0", monkeypatch)
+    b, acc_b, _, _ = _run_c3(tmp_path, "1", monkeypatch)
+    assert torch.equal(a["sup"], b["sup"])
+    assert torch.equal(a["q_emb"], b["q_emb"])
+    assert torch.equal(a["pred"], b["pred"]) and acc_a == acc_b

@@ -59,11 +59,16 @@ def config3(args):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     acc = float(np.mean([p == q["query_y"] for p, q in zip(preds, plans)]))
-    frames_ep = 16 + 5 * 16 + 40 * 16  # query (<=16) + supports + 40 augmented clips
+    reforward = os.environ.get("EOSV_AUG_REFORWARD", "0") == "1"
+    # backbone frames per episode: query (<=16) + 5 supports x 16 (+ 40 augmented clips x 16 when
+    # they are re-forwarded as the reference does; by default their features are gathered)
+    frames_ep = 16 + 5 * 16 + (40 * 16 if reforward else 0)
     gflop = 2 * arch.conv_macs_per_frame(arch.SPECS["resnet50"]) / 1e9
     return {"config": "3: test_network_aug_segment aug_seg_T 5w1s R50 224 (drop-in TestNetwork)",
-            "dtype": args.dtype, "episodes": args.episodes, "episodes_per_s": round(args.episodes / el, 2),
-            "clips_per_s": round(args.episodes * 46 / el, 1), "frames_per_s": round(args.episodes * frames_ep / el, 1),
+            "dtype": args.dtype, "aug_features": "reforward" if reforward else "gathered",
+            "episodes": args.episodes, "batch": B, "episodes_per_s": round(args.episodes / el, 2),
+            "clips_per_s": round(args.episodes * 46 / el, 1),
+            "backbone_frames_per_episode": frames_ep, "backbone_frames_per_s": round(args.episodes * frames_ep / el, 1),
             "end_to_end_tflops": round(args.episodes * frames_ep * gflop / el / 1e3, 1),
             "gallery_s": round(t_gal, 3), "gallery_frames": 10240, "episode_acc": acc}
 
@@ -73,7 +78,7 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--episodes", type=int, default=64)
-    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
     if args.config == 3:
