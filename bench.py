@@ -139,15 +139,15 @@ def measured_traffic(dtype):
     return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
 
 
-def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches):
+def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches, chunks):
     """Conv-family algorithmic bytes per launch: every layer's input + output (+ residual) map
-    once per frame and its weights once per launch (arch.conv_layer_bytes)."""
+    once per frame and its weights once per chunk (arch.conv_layer_bytes: the unfused plan's
+    floor; with the downsample folded into the block's last conv there are fewer launches)."""
     elem = 2 if dtype == "bf16" else 4
     layers = arch_mod.conv_layer_bytes(arch_mod.SPECS[args.arch], args.res, args.res, elem,
                                        stem_pool_fused=(dtype == "bf16"))
     per_frame = sum(b for b, _ in layers)
     weights = sum(w for _, w in layers)
-    chunks = launches / len(layers)
     return (frames * per_frame + chunks * weights) / launches
 
 
@@ -164,7 +164,8 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
         tr, src = measured_traffic(dtype)
         out["traffic"] = tr
         out["traffic_unit"] = "HBM bytes per conv launch"
-        out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, int(nl.sum())))
+        out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, int(nl.sum()),
+                                                                        int(nl[0])))
         out["traffic_source"] = src
     return out
 

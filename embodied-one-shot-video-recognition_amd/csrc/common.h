@@ -46,6 +46,10 @@ struct ConvArgs {
   int abl;            // ablation bits for profiling builds (0 = normal)
   int xcd;            // 1: XCD-aware block order (each XCD walks a contiguous range of tiles)
   int kcm;            // bf16 only: K ordered (cin/64, kh, kw, cin%64) instead of (kh, kw, cin)
+  // fused 1x1 downsample (ResNet block shortcut): K columns [K1, K) read x2 at output pixel
+  // (oh, ow) -> x2 pixel (oh * stride2, ow * stride2), channel k - K1; nullptr = none
+  const void* x2;     // NHWC [N, H2, W2, Cin2]
+  int H2, W2, Cin2, stride2, K1;
 };
 
 // Workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one L2;

@@ -29,7 +29,7 @@ __device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__
 
 // MF = MFMA tile edge: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16; same
 // cycles per FLOP, but the chip holds a higher clock on it with random operands)
-template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS>
+template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BK = 64;  // bf16 elements per row = 128 B
   constexpr int NW = WM * WN;
@@ -62,6 +62,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int pc = lane & 7;
   const int xrow = ((a.W + 2 * a.pad + 1) & ~1) * 3;  // STEM: elements per padded input row
   const u16* arow[AI];
+  const u16* arow2[DS ? AI : 1];  // DS: the fused downsample's input pixel (always in bounds)
   int aih[AI], aiw[AI], alc[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
@@ -81,11 +82,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         arow[j] = x + ((long long)img * (a.H + 2 * a.pad) + oh * a.stride) * xrow + (long long)ow * a.stride * 3;
       } else {
         arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 8;
+        if constexpr (DS)
+          arow2[j] = (const u16*)a.x2 +
+                     (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 + lc * 8;
       }
     } else {
       aih[j] = -(1 << 28);
       aiw[j] = 0;
       arow[j] = x;
+      if constexpr (DS) arow2[j] = nullptr;
     }
   }
   const u16* brow[BI];
@@ -101,6 +106,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     u16* As = smem + slot * STAGE;
     u16* Bs = As + BM * BK;
     if (skip & 4) {
+    } else if (DS && k0 >= a.K1) {
+#pragma unroll
+      for (int j = 0; j < (DS ? AI : 1); ++j) {
+        const u16* src = arow2[j] ? arow2[j] + (k0 - a.K1) : zero;
+        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
     } else if constexpr (STEM) {
 #pragma unroll
       for (int j = 0; j < AI; ++j) {
@@ -323,10 +335,17 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
-  if (bf16_mfma() == 32)
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 32, NS>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s, a);
+  if (a.x2) {
+    if (STEM || a.K1 % 64 || a.Cin2 % 64) return set_error("conv_bf16: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
+                       s, a);
+  } else if (bf16_mfma() == 32) {
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 32, NS, false>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
+                       s, a);
+  } else {
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS, false>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
+                       s, a);
+  }
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -361,7 +380,7 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
-  if (bf16_rows() && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  if (bf16_rows() && !a.x2 && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
   if (bf16_p8() && conv_bf16_p8_ok(a) && (bf16_p8() == 2 || conv_bf16_p8_default(a))) return launch_conv_bf16_p8(a, s);
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
   // K = 64 1x1 convs all measured slower than this choice

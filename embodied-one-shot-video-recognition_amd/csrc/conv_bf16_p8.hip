@@ -36,7 +36,7 @@ __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
 }  // namespace
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool DS>
 __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
   constexpr int BK = 64;
   constexpr int NW = 8;
@@ -75,6 +75,13 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
       (void*)(x + (long long)img0 * a.H * a.W * a.Cin), (short)0, (int)((img1 - img0 + 1) * img_bytes), 0x00020000);
   int aoffs[AI];
   unsigned amask[AI];
+  // DS: the fused 1x1 downsample's input rows (K columns [K1, K)), same image range
+  __amdgpu_buffer_rsrc_t xr2 = xr;
+  int aoffs2[DS ? AI : 1];
+  if constexpr (DS)
+    xr2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const u16*)a.x2 + (long long)img0 * a.H2 * a.W2 * a.Cin2), (short)0,
+        (int)((long long)(img1 - img0 + 1) * a.H2 * a.W2 * a.Cin2 * 2), 0x00020000);
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
     const int row = wid * (BM / NW) + 8 * j + lr;
@@ -82,6 +89,7 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
     const int m = m0 + row;
     amask[j] = 0;
     aoffs[j] = 0;
+    if constexpr (DS) aoffs2[j] = -1;
     if (m < M) {
       const int img = m / HoWo;
       const int rem = m - img * HoWo;
@@ -89,6 +97,8 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
       const int ow = rem - oh * a.Wo;
       const int ih = oh * a.stride - a.pad, iw = ow * a.stride - a.pad;
       aoffs[j] = (((img - img0) * a.H + ih) * a.W + iw) * a.Cin * 2 + lc * 16;
+      if constexpr (DS)
+        aoffs2[j] = (((img - img0) * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 * 2 + lc * 16;
       for (int kh = 0; kh < a.KH; ++kh)
         for (int kw = 0; kw < a.KW; ++kw)
           if ((unsigned)(ih + kh) < (unsigned)a.H && (unsigned)(iw + kw) < (unsigned)a.W) amask[j] |= 1u << (kh * a.KW + kw);
@@ -104,7 +114,7 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
   }
   // K walk kept incrementally: tap index (kh * KW + kw), kw, channel offset c0 and the tap's
   // byte offset; K order (kh, kw, cin) or, with a.kcm, (cin / 64, kh, kw, cin % 64)
-  int tap = 0, toff = 0, kwc = 0, c0 = 0;
+  int tap = 0, toff = 0, kwc = 0, c0 = 0, kk = 0;
   const int taps = a.KH * a.KW;
   const int row_step = (a.W - a.KW) * a.Cin * 2;  // bytes from tap (kh, KW-1) + Cin to (kh+1, 0)
   auto next_tap = [&]() {
@@ -116,6 +126,7 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
     }
   };
   auto advance = [&]() {
+    kk += BK;
     if (a.kcm) {
       next_tap();
       if (tap == taps) {
@@ -135,6 +146,16 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
     }
   };
   auto stage_a = [&](u16* As) {
+    if (DS && kk >= a.K1) {
+      const int d = (kk - a.K1) * 2;
+#pragma unroll
+      for (int j = 0; j < (DS ? AI : 1); ++j) {
+        const int voff = aoffs2[j] >= 0 ? aoffs2[j] + d : (int)0x80000000;
+        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const int voff = ((amask[j] >> tap) & 1) ? aoffs[j] + toff : (int)0x80000000;
@@ -349,6 +370,7 @@ bool conv_bf16_p8_ok(const ConvArgs& a) {
 // stride-1 Cout = 128 convs (+1-3 %); at Cout >= 256 it ties conv_bf16_kernel's 256x256 tile and
 // on the stride-2 / 1x1 entries it is 5-10 % slower.  EOSV_BF16_P8=2 routes every eligible conv.
 bool conv_bf16_p8_default(const ConvArgs& a) { return a.Cout == 128 && a.stride == 1 && a.K >= 576; }
+// (with a fused downsample, a.K includes its Cin2 columns; the shape test above is unchanged)
 
 int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s) {
   if (!conv_bf16_p8_ok(a)) return set_error("conv_bf16_p8: unsupported shape"), EOSV_ERR_UNSUPPORTED;
@@ -357,10 +379,18 @@ int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s) {
   const int BN = a.Cout == 128 ? 128 : 256;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv_bf16_p8: grid too large"), EOSV_ERR_UNSUPPORTED;
-  if (a.Cout == 128)
-    hipLaunchKernelGGL((conv_bf16_p8_kernel<512, 128, 4, 2>), dim3((unsigned)nb), dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_bf16_p8_kernel<256, 256, 2, 4>), dim3((unsigned)nb), dim3(512), 0, s, a);
+  if (a.x2 && (a.K1 % 64 || a.Cin2 % 64)) return set_error("conv_bf16_p8: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
+  if (a.Cout == 128) {
+    if (a.x2)
+      hipLaunchKernelGGL((conv_bf16_p8_kernel<512, 128, 4, 2, true>), dim3((unsigned)nb), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_bf16_p8_kernel<512, 128, 4, 2, false>), dim3((unsigned)nb), dim3(512), 0, s, a);
+  } else {
+    if (a.x2)
+      hipLaunchKernelGGL((conv_bf16_p8_kernel<256, 256, 2, 4, true>), dim3((unsigned)nb), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_bf16_p8_kernel<256, 256, 2, 4, false>), dim3((unsigned)nb), dim3(512), 0, s, a);
+  }
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

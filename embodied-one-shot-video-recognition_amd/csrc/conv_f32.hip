@@ -196,6 +196,7 @@ int launch_conv_f32(const ConvArgs& a, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   const int impl = a.zero ? conv_impl() : 1;
+  if (a.x2 && impl == 1) return set_error("conv_f32: fused downsample needs the DMA kernel"), EOSV_ERR_UNSUPPORTED;
   if (impl == 1 && !stem) {
     if (a.Cout <= 64) return launch_v1<128, 64>(a, s);
     return launch_v1<128, 128>(a, s);

@@ -29,7 +29,7 @@ namespace eosv {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS, bool EPI_LDS>
+template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS, bool EPI_LDS, bool DS>
 __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 32;
@@ -64,6 +64,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   const int pc = lane % CPR;
   // per staged A row: pointer at pixel (ih0, iw0) + this lane's logical chunk, and ih0/iw0
   const float* arow[AI];
+  const float* arow2[DS ? AI : 1];  // DS: the fused downsample's input pixel (always in bounds)
   int aih[AI], aiw[AI];
   const int xrow = ((a.W + 2 * a.pad + 1) & ~1) * 3;  // STEM: floats per padded input row
 #pragma unroll
@@ -84,11 +85,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
         arow[j] = x + ((long long)img * (a.H + 2 * a.pad) + oh * a.stride) * xrow + (long long)ow * a.stride * 3;
       } else {
         arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 4;
+        if constexpr (DS)
+          arow2[j] = (const float*)a.x2 +
+                     (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 + lc * 4;
       }
     } else {
       aih[j] = -(1 << 28);
       aiw[j] = 0;
       arow[j] = x;
+      if constexpr (DS) arow2[j] = nullptr;
     }
   }
   const float* brow[BI];
@@ -110,6 +115,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
         const int kh = g / 6;
         const bool ok = aih[j] > -(1 << 27) && kh < a.KH;
         const float* src = ok ? arow[j] + kh * xrow + (g - 6 * kh) * 4 : zero;
+        float* dst = As + (wid * (BM / NW) + RPI * j) * BK;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
+    } else if (DS && k0 >= a.K1) {
+#pragma unroll
+      for (int j = 0; j < (DS ? AI : 1); ++j) {
+        const float* src = arow2[j] ? arow2[j] + (k0 - a.K1) : zero;
         float* dst = As + (wid * (BM / NW) + RPI * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
@@ -274,8 +286,14 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS, EPI>), dim3((unsigned)nb), dim3(64 * WM * WN), 0, s,
-                     a);
+  if (a.x2) {
+    if (STEM || a.K1 % BK || a.Cin2 % BK) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, false, NS, EPI, true>), dim3((unsigned)nb),
+                       dim3(64 * WM * WN), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS, EPI, false>), dim3((unsigned)nb),
+                       dim3(64 * WM * WN), 0, s, a);
+  }
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

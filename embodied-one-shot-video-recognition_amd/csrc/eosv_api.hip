@@ -9,6 +9,7 @@
 #include <hip/hip_bf16.h>
 
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -25,6 +26,7 @@ struct Conv {
   int cin = 0, cout = 0, kh = 1, kw = 1, kwp = 1, cinp = 0, stride = 1, pad = 0, K = 0;
   bool stem = false;
   bool kcm = false;           // bf16 weights in chunk-major K order (ConvArgs::kcm)
+  int kds = 0;                // fused downsample: extra K columns (its Cin) after this conv's K
   int id = 0;                 // layer id for profiling (plan order)
   std::string wname, bnname;  // state_dict prefixes
   void* w = nullptr;          // [cout][K] (f32 or bf16)
@@ -33,6 +35,7 @@ struct Conv {
 
 struct Block {
   bool bottleneck = false, has_ds = false;
+  bool fuse_ds = false;  // downsample folded into the last conv's K (ConvArgs::x2), no ds launch
   Conv c1, c2, c3, ds;
 };
 
@@ -86,6 +89,17 @@ static Conv make_conv(int cin, int cout, int k, int stride, int pad, const std::
   c.wname = wname;
   c.bnname = bnname;
   return c;
+}
+
+// The block shortcut's 1x1 downsample conv (+ its folded BN) becomes extra K columns of the
+// block's last conv: out = relu(W_last . h + W_ds . x_strided + b_last + b_ds), one launch
+// instead of two and no residual round trip through HBM.  EOSV_FUSE_DS=0: separate launch.
+static bool fuse_ds_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("EOSV_FUSE_DS");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
 }
 
 static int build_plan(eosv_handle* h) {
@@ -147,6 +161,8 @@ static int build_plan(eosv_handle* h) {
       if (bi == 0 && (s != 1 || inpl != cout)) {
         b.has_ds = true;
         b.ds = make_conv(inpl, cout, 1, s, 0, p + ".downsample.0.weight", p + ".downsample.1");
+        b.fuse_ds = fuse_ds_enabled();
+        if (b.fuse_ds) (bottleneck ? b.c3 : b.c2).kds = inpl;
       }
       h->blocks.push_back(b);
       hh = ho;
@@ -213,17 +229,20 @@ struct Tensors {
   }
 };
 
-// fold BN (eval) into the conv and upload [cout][K] weights + [cout] bias
-static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, bool has_bn) {
+// fold BN (eval) into the conv: host [cout][K] weights (K order as the kernels read it) and
+// [cout] shift.  False (error set) on a missing tensor.
+static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::vector<float>& wf,
+                      std::vector<float>& beta) {
   const float* w = t.get(c.wname, (int64_t)c.cout * c.cin * c.kh * c.kw);
-  if (!w) return EOSV_ERR_ARG;
-  std::vector<float> alpha(c.cout, 1.f), beta(c.cout, 0.f);
+  if (!w) return false;
+  std::vector<float> alpha(c.cout, 1.f);
+  beta.assign(c.cout, 0.f);
   if (has_bn) {
     const float* g = t.get(c.bnname + ".weight", c.cout);
     const float* bb = t.get(c.bnname + ".bias", c.cout);
     const float* mu = t.get(c.bnname + ".running_mean", c.cout);
     const float* var = t.get(c.bnname + ".running_var", c.cout);
-    if (!g || !bb || !mu || !var) return EOSV_ERR_ARG;
+    if (!g || !bb || !mu || !var) return false;
     for (int o = 0; o < c.cout; ++o) {
       // same arithmetic as torch's CPU BN inference: alpha = gamma / sqrt(var + eps)
       alpha[o] = (1.f / std::sqrt(var[o] + 1e-5f)) * g[o];
@@ -231,14 +250,14 @@ static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, boo
     }
   } else if (!c.bnname.empty()) {
     const float* bias = t.get(c.bnname, c.cout);
-    if (!bias) return EOSV_ERR_ARG;
+    if (!bias) return false;
     for (int o = 0; o < c.cout; ++o) beta[o] = bias[o];
   }
   // bf16 multi-tap convs with Cin > 64: K chunk-major, (cin / 64, kh, kw, cin % 64), so that a
   // conv's K walk visits all taps of one 64-channel slice of the input before the next slice
-  // and the block's input patch is re-read from L2, not from beyond it (conv_bf16_p8.hip)
+  // (conv_bf16_p8.hip)
   c.kcm = bf16 && !c.stem && c.cinp % 64 == 0 && c.cinp > 64 && c.kh * c.kw > 1 && c.kwp == c.kw;
-  std::vector<float> wf((size_t)c.cout * c.K, 0.f);
+  wf.assign((size_t)c.cout * c.K, 0.f);
   for (int o = 0; o < c.cout; ++o)
     for (int i = 0; i < c.cin; ++i)
       for (int y = 0; y < c.kh; ++y)
@@ -248,6 +267,27 @@ static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, boo
                                  : ((size_t)y * c.kwp + x) * c.cinp + i;
           wf[(size_t)o * c.K + k] = v * alpha[o];
         }
+  return true;
+}
+
+// upload [cout][K (+ ds K)] weights + [cout] bias; with `ds`, the downsample's folded 1x1
+// weights are appended as K columns [c.K, c.K + ds.cin) and its shift is added to the bias
+static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, bool has_bn, Conv* ds = nullptr) {
+  std::vector<float> wf, beta;
+  if (!fold_conv(c, t, bf16, has_bn, wf, beta)) return EOSV_ERR_ARG;
+  if (ds) {
+    std::vector<float> wd, bd;
+    if (!fold_conv(*ds, t, bf16, true, wd, bd)) return EOSV_ERR_ARG;
+    if (ds->cout != c.cout || ds->kh != 1 || ds->K != c.kds) return set_error("fused downsample shape"), EOSV_ERR_ARG;
+    const int Kt = c.K + c.kds;
+    std::vector<float> wc((size_t)c.cout * Kt);
+    for (int o = 0; o < c.cout; ++o) {
+      std::copy(wf.begin() + (size_t)o * c.K, wf.begin() + (size_t)(o + 1) * c.K, wc.begin() + (size_t)o * Kt);
+      std::copy(wd.begin() + (size_t)o * c.kds, wd.begin() + (size_t)(o + 1) * c.kds, wc.begin() + (size_t)o * Kt + c.K);
+      beta[o] += bd[o];
+    }
+    wf.swap(wc);
+  }
   int rc;
   if (bf16) {
     std::vector<unsigned short> wb(wf.size());
@@ -273,7 +313,8 @@ static hipEvent_t prof_event(eosv_handle* h) {
 }
 
 static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, int W, const void* res,
-                    void* y, bool relu, bool bf16, hipStream_t s) {
+                    void* y, bool relu, bool bf16, hipStream_t s, const void* x2 = nullptr, int H2 = 0,
+                    int W2 = 0, int stride2 = 1) {
   ConvArgs a{};
   a.x = x;
   a.w = c.w;
@@ -292,8 +333,16 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   a.KWp = c.kwp;
   a.stride = c.stride;
   a.pad = c.pad;
-  a.K = c.K;
+  a.K = c.K + (x2 ? c.kds : 0);
   a.relu = relu ? 1 : 0;
+  if (x2) {  // fused downsample: K columns [c.K, c.K + kds) read x2 (1x1, stride2)
+    a.x2 = x2;
+    a.H2 = H2;
+    a.W2 = W2;
+    a.Cin2 = c.kds;
+    a.stride2 = stride2;
+    a.K1 = c.K;
+  }
   a.zero = h->zero;
   static const int xcd = [] {
     const char* e = getenv("EOSV_XCD");  // 0 = plain blockIdx order (A/B switch)
@@ -311,7 +360,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   const int rc = bf16 ? launch_conv_bf16(a, s) : launch_conv_f32(a, s);
   if (h->prof && rc == EOSV_OK) {
     EOSV_HIP_CHECK(hipEventRecord(e1, s));
-    const double macs = (double)N * a.Ho * a.Wo * c.cout * c.kh * c.kw * c.cin;
+    const double macs = (double)N * a.Ho * a.Wo * c.cout * ((double)c.kh * c.kw * c.cin + (x2 ? c.kds : 0));
     h->recs.push_back({c.id, e0, e1, 2.0 * macs});
   }
   return rc;
@@ -331,19 +380,23 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
       if (bufs[k] != x) fr[nf++] = bufs[k];
     const int st = b.bottleneck ? b.c2.stride : b.c1.stride;  // torchvision: stride on the 3x3
     const int ho = conv_out(hh, 3, st, 1), wo = conv_out(ww, 3, st, 1);
-    void* r = x;
-    if (b.has_ds) {
+    void* r = x;  // residual: the block input, or the downsample's output
+    if (b.has_ds && !b.fuse_ds) {
       r = fr[2];
       if ((rc = run_conv(h, b.ds, x, B, hh, ww, nullptr, r, false, bf, s))) return rc;
     }
-    void* y = (dst && bi + 1 == b1) ? dst : r;
+    void* y = (dst && bi + 1 == b1) ? dst : (b.has_ds ? fr[2] : r);
+    // fused downsample: the last conv reads x (strided) as extra K columns, no residual
+    const void* res = b.fuse_ds ? nullptr : r;
+    const void* x2 = b.fuse_ds ? x : nullptr;
+    const int s2 = b.has_ds ? b.ds.stride : 1;
     if (!b.bottleneck) {
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
-      if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, r, y, true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) return rc;
     } else {
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
       if ((rc = run_conv(h, b.c2, fr[0], B, hh, ww, nullptr, fr[1], true, bf, s))) return rc;
-      if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, r, y, true, bf, s))) return rc;
+      if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) return rc;
     }
     x = y;
     hh = ho;
@@ -485,9 +538,10 @@ int eosv_load_weights(eosv_handle* h, const char* const* names, const void* cons
   if ((rc = upload_conv(h, h->stem, t, bf, true))) return rc;
   for (Block& b : h->blocks) {
     if ((rc = upload_conv(h, b.c1, t, bf, true))) return rc;
-    if ((rc = upload_conv(h, b.c2, t, bf, true))) return rc;
-    if (b.bottleneck && (rc = upload_conv(h, b.c3, t, bf, true))) return rc;
-    if (b.has_ds && (rc = upload_conv(h, b.ds, t, bf, true))) return rc;
+    Conv* fds = b.fuse_ds ? &b.ds : nullptr;
+    if ((rc = upload_conv(h, b.c2, t, bf, true, b.bottleneck ? nullptr : fds))) return rc;
+    if (b.bottleneck && (rc = upload_conv(h, b.c3, t, bf, true, fds))) return rc;
+    if (b.has_ds && !b.fuse_ds && (rc = upload_conv(h, b.ds, t, bf, true))) return rc;
   }
   Conv& fc = h->fc;
   fc.bnname = "fc.bias";
