@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-baseline-sec", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
+    ap.add_argument("--config-label", default="BASELINE configs[1]",
+                    help="which BASELINE.json config this run measures (tools/bench_configs.py sets it)")
     ap.add_argument("--secondary-dtype", default="bf16",
                     help="also time the same episodes with this backbone dtype ('' to skip)")
     return ap.parse_args()
@@ -124,17 +126,18 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     return edist.max_over_ranks(elapsed), torch.cat(preds), prof
 
 
-def measured_traffic(dtype):
+def measured_traffic(dtype, key):
     """HBM bytes per conv launch from the newest profiles/<tag>_traffic.json (written by
     tools/prof_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-    same command); EOSV_TRAFFIC_PROFILE names a specific file.  None if there is none."""
+    same command); EOSV_TRAFFIC_PROFILE names a specific file.  None if there is none or it was
+    measured on another workload (key = arch@HxW)."""
     import glob
     path = os.environ.get("EOSV_TRAFFIC_PROFILE") or \
         (sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))) or [None])[-1]
     if not path or not os.path.exists(path):
         return None, None
     d = json.load(open(path))
-    if dtype not in d:
+    if dtype not in d or d.get("key") != key:
         return None, None
     return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
 
@@ -161,7 +164,7 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
            "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
                      f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
     if args is not None and nl.sum() > 0:
-        tr, src = measured_traffic(dtype)
+        tr, src = measured_traffic(dtype, f"{args.arch}@{args.res}x{args.res}")
         out["traffic"] = tr
         out["traffic_unit"] = "HBM bytes per conv launch"
         out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, int(nl.sum()),
@@ -237,7 +240,7 @@ def main():
                     "reference architecture; episodes from the reference's test.list in its RNG order",
             "config": {"workload": f"test_network_baseline {args.n_way}-way {args.k_shot}-shot, "
                                    f"{args.segments} seg x {args.seg_len} frames, {args.arch}, "
-                                   f"{args.res}x{args.res}, {args.dtype} (BASELINE configs[1])",
+                                   f"{args.res}x{args.res}, {args.dtype} ({args.config_label})",
                        "episodes_per_step_per_gpu": E, "episodes_timed": E * args.steps * world,
                        "frames_per_clip": T, "parallelism": f"episode-sharded dp{world}"},
             "frames_per_s": round(frames / elapsed, 1),

@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--episodes", type=int, default=64)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--max-frames", type=int, default=2048, help="backbone chunk (configs 4 / 5)")
     args = ap.parse_args()
     if args.config == 3:
         print(json.dumps(config3(args)), flush=True)
@@ -88,7 +89,7 @@ def main():
              5: ["--arch", "resnet101", "--n-way", "5", "--k-shot", "5", "--segments", "32", "--res", "256"]}[args.config]
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), *shape, "--dtype", args.dtype,
            "--episodes-per-step", str(args.episodes), "--steps", "2", "--no-cpu-baseline", "--secondary-dtype", "",
-           "--max-frames", "512"]
+           "--max-frames", str(args.max_frames), "--config-label", f"BASELINE configs[{args.config - 1}]"]
     sys.exit(subprocess.call(cmd))
 
 

@@ -102,5 +102,10 @@ for fam, keys in FAMILIES.items():
         traffic[fam] = {"launches": n["FETCH_SIZE"],
                         "hbm_bytes_per_launch": round((2 * tot["FETCH_SIZE"] / n["FETCH_SIZE"] +
                                                        tot["WRITE_SIZE"] / n["WRITE_SIZE"]) * 1024)}
+if bench:  # the workload these counters belong to (bench.py attaches them only to the same one)
+    import re
+    mm = re.search(r"(resnet\d+), (\d+)x(\d+)", bench["config"]["workload"])
+    if mm:
+        traffic["key"] = f"{mm.group(1)}@{mm.group(2)}x{mm.group(3)}"
 open(f"{dst}/{tag}_traffic.json", "w").write(json.dumps(traffic, indent=1) + "\n")
 print("\n".join(out))
