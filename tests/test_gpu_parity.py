@@ -189,3 +189,50 @@ def test_normalize_frames_bit_exact_vs_host_transform():
     a = rgb[:, top:top + 224, left:left + 224].astype(np.float32) / np.float32(255.0)
     ref = ((a - fr.MEAN) / fr.STD).transpose(0, 3, 1, 2)
     assert np.array_equal(out.view(np.uint32), np.ascontiguousarray(ref).view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype,name", [("f32", "resnet18"), ("bf16", "resnet18"), ("bf16", "resnet50"),
+                                        ("f32", "resnet50")])
+def test_backbone_batch_invariance(dtype, name):
+    """A frame's features do not depend on its batch, its position in it or the chunking
+    (bit-exact): every kernel computes a frame with the same instruction sequence wherever it
+    sits.  The config-3 feature gather (network_test.gallery_features) relies on this."""
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    x = torch.randn(37, 3, 224, 224, generator=torch.Generator().manual_seed(5)).cuda()
+    big = engine.Backbone(name, dtype, 224, 224, max_frames=37)
+    big.load_state_dict(sd)
+    a = big.forward(x)
+    big.close()
+    small = engine.Backbone(name, dtype, 224, 224, max_frames=8)  # 5 chunks, ragged tail
+    small.load_state_dict(sd)
+    b = small.forward(x)
+    c = torch.cat([small.forward(x[:13].contiguous()), small.forward(x[13:].contiguous())])
+    d = small.forward(x[21:22].contiguous())
+    small.close()
+    assert torch.equal(a, b) and torch.equal(a, c)
+    assert torch.equal(a[21:22], d)
+
+
+def test_full_size_c2_f32_bf16_agreement():
+    """Config 2 at its full shape (224², T=16, R18, 400 episodes = 38,400 frames through
+    the chunked forward): f32 and bf16 predict the same class on >= 97 % of the episodes,
+    and both predict within the episode's 5 support classes; f32 episode accuracy equals the
+    mean of its 0/1 correctness (the reference's avg_acc, exact)."""
+    from eosv import episodes as ep_mod
+    plans = ep_mod.sample_episodes(400, 5, 1, "test", seed=17)
+    b = engine.build_episode_batch(plans, T=16)
+    dev = engine.DeviceEpisodes(b, 224, 224)
+    preds = {}
+    for dt in ("f32", "bf16"):
+        bb = engine.Backbone("resnet18", dt, 224, 224, max_frames=4096)
+        bb.load_state_dict(synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0))
+        p, emb, _ = engine.run_episodes(bb, dev, "protonet", True)
+        preds[dt] = p.cpu().numpy()
+        assert torch.isfinite(emb).all()
+        bb.close()
+    assert ((preds["f32"] >= 0) & (preds["f32"] < 5)).all()
+    agree = (preds["f32"] == preds["bf16"]).mean()
+    assert agree >= 0.97, agree
+    qy = np.array([p["query_y"] for p in plans])
+    acc = (preds["f32"] == qy).mean()
+    assert 0.2 < acc <= 1.0
