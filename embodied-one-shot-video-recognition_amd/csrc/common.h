@@ -69,6 +69,9 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 bool stem_pool_bf16_ok(int H, int W);  // stem_pool_bf16.hip: fused stem conv + ReLU + maxpool
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                           hipStream_t s);
+bool stem_pool_f32_ok(int H, int W);  // stem_pool_f32.hip: the same for f32
+int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
+                         hipStream_t s);
 bool conv_bf16_p8_ok(const ConvArgs& a);  // conv_bf16_p8.hip: phased 8-wave implicit GEMM
 bool conv_bf16_p8_default(const ConvArgs& a);
 int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s);

@@ -406,12 +406,16 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
   return EOSV_OK;
 }
 
-static bool stem_pool_fused() {
-  static const bool v = [] {
+static bool stem_pool_fused(bool bf) {
+  static const bool vb = [] {
     const char* e = getenv("EOSV_BF16_STEMPOOL");  // 0 = separate stem conv + maxpool (A/B switch)
     return !e || atoi(e) != 0;
   }();
-  return v;
+  static const bool vf = [] {
+    const char* e = getenv("EOSV_F32_STEMPOOL");  // 0 = separate stem conv + maxpool (A/B switch)
+    return !e || atoi(e) != 0;
+  }();
+  return bf ? vb : vf;
 }
 
 // stem -> maxpool -> stage-0 blocks for frames [0, B) of `frames`, output into `dst`
@@ -420,7 +424,7 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
   const int H = h->d.height, W = h->d.width;
   int rc;
   if ((rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, bf, s))) return rc;
-  if (bf && stem_pool_fused() && stem_pool_bf16_ok(H, W)) {
+  if (stem_pool_fused(bf) && (bf ? stem_pool_bf16_ok(H, W) : stem_pool_f32_ok(H, W))) {
     // fused stem conv + ReLU + maxpool (profiled as the stem layer)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) {
@@ -429,7 +433,9 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
       if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
       EOSV_HIP_CHECK(hipEventRecord(e0, s));
     }
-    if ((rc = launch_stem_pool_bf16(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s))) return rc;
+    if ((rc = bf ? launch_stem_pool_bf16(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s)
+                 : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s)))
+      return rc;
     if (h->prof) {
       EOSV_HIP_CHECK(hipEventRecord(e1, s));
       h->recs.push_back({h->stem.id, e0, e1, 2.0 * B * h->hs * h->ws * 64 * 147});

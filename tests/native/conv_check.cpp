@@ -231,11 +231,79 @@ static int check_stem_pool(int N, int H, int W) {
   return bad || rc ? 1 : 0;
 }
 
+// fused f32 stem + shift + ReLU + maxpool vs a double reference on the same f32 operands
+// (weights in the uploaded [64][176] = [kh 7][24] + 8 layout)
+static int check_stem_pool_f32(int N, int H, int W) {
+  const int pad = 3, Wp = stem_row_pixels(W, pad), Hp = H + 2 * pad;
+  const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
+  const int Hq = (Hs - 1) / 2 + 1, Wq = (Ws - 1) / 2 + 1;
+  unsigned s = 5151;
+  std::vector<float> x(stem_input_elems(N, H, W, pad) + 64, 0.f), w(64 * 176, 0.f), b(64);
+  for (int n = 0; n < N; ++n)
+    for (int i = 0; i < H; ++i)
+      for (int j = 0; j < W; ++j)
+        for (int c = 0; c < 3; ++c) x[(((size_t)n * Hp + i + pad) * Wp + j + pad) * 3 + c] = frand(s);
+  for (int o = 0; o < 64; ++o)
+    for (int kh = 0; kh < 7; ++kh)
+      for (int kw = 0; kw < 7; ++kw)
+        for (int c = 0; c < 3; ++c) w[o * 176 + kh * 24 + kw * 3 + c] = frand(s) * 0.2f;
+  for (auto& v : b) v = frand(s) * 0.5f;
+  float *dx, *dw, *dy, *db;
+  const size_t ny = (size_t)N * Hq * Wq * 64;
+  hipMalloc(&dx, x.size() * 4); hipMalloc(&dw, w.size() * 4); hipMalloc(&dy, ny * 4); hipMalloc(&db, 64 * 4);
+  hipMemcpy(dx, x.data(), x.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dw, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db, b.data(), 64 * 4, hipMemcpyHostToDevice);
+  hipMemset(dy, 0xff, ny * 4);
+  const int rc = launch_stem_pool_f32(dx, N, H, W, dw, db, dy, 0);
+  hipDeviceSynchronize();
+  std::vector<float> y(ny);
+  hipMemcpy(y.data(), dy, ny * 4, hipMemcpyDeviceToHost);
+  std::vector<double> st((size_t)Hs * Ws * 64);
+  long bad = 0;
+  double maxerr = 0;
+  for (int n = 0; n < N; ++n) {
+    for (int sy = 0; sy < Hs; ++sy)
+      for (int sx = 0; sx < Ws; ++sx)
+        for (int o = 0; o < 64; ++o) {
+          double acc = b[o];
+          for (int kh = 0; kh < 7; ++kh)
+            for (int kw = 0; kw < 7; ++kw)
+              for (int c = 0; c < 3; ++c)
+                acc += (double)x[(((size_t)n * Hp + 2 * sy + kh) * Wp + 2 * sx + kw) * 3 + c] * w[o * 176 + kh * 24 + kw * 3 + c];
+          st[((size_t)sy * Ws + sx) * 64 + o] = acc > 0 ? acc : 0;
+        }
+    for (int py = 0; py < Hq; ++py)
+      for (int px = 0; px < Wq; ++px)
+        for (int o = 0; o < 64; ++o) {
+          double m = -INFINITY;
+          for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+              const int sy = 2 * py + dy, sx = 2 * px + dx;
+              if (sy >= 0 && sy < Hs && sx >= 0 && sx < Ws) m = fmax(m, st[((size_t)sy * Ws + sx) * 64 + o]);
+            }
+          const float got = y[(((size_t)n * Hq + py) * Wq + px) * 64 + o];
+          const double e = fabs(got - m);
+          if (!(e <= 1e-5 * (1 + fabs(m)))) {
+            if (bad < 5) printf("  bad n%d py%d px%d o%d ref %f got %f\n", n, py, px, o, m, got);
+            ++bad;
+          }
+          maxerr = fmax(maxerr, e);
+        }
+  }
+  printf("%s stem_pool f32 N%d H%d W%d rc=%d maxerr %.3e bad %ld\n", bad ? "FAIL" : "ok  ", N, H, W, rc, maxerr, bad);
+  hipFree(dx); hipFree(dw); hipFree(dy); hipFree(db);
+  return bad || rc ? 1 : 0;
+}
+
 int main() {
   int fails = 0;
   fails += check_stem_pool(2, 224, 224);
   fails += check_stem_pool(3, 100, 86);  // ragged: partial last column tile, odd pooled sizes
   fails += check_stem_pool(2, 64, 48);
+  fails += check_stem_pool_f32(2, 224, 224);
+  fails += check_stem_pool_f32(3, 100, 86);
+  fails += check_stem_pool_f32(2, 64, 48);
   // stage-1 shape (row-strip kernel): 300 images = 4200 strips, several strips per workgroup
   fails += check_bf16(300, 56, 56, 64, 64, 3, 1, 1, true, true);
   fails += check_bf16(3, 56, 56, 64, 64, 3, 1, 1, false, true);
