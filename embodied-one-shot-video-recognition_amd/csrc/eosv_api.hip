@@ -423,8 +423,15 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
                      bool bf, hipStream_t s) {
   const int H = h->d.height, W = h->d.width;
   int rc;
-  if ((rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, bf, s))) return rc;
-  if (stem_pool_fused(bf) && (bf ? stem_pool_bf16_ok(H, W) : stem_pool_f32_ok(H, W))) {
+  static const bool direct = [] {
+    const char* e = getenv("EOSV_STEM_DIRECT");  // 0 = pack kernel + LDS-DMA rows (A/B switch)
+    return !e || atoi(e) != 0;
+  }();
+  const bool fused = stem_pool_fused(bf) && (bf ? stem_pool_bf16_ok(H, W) : stem_pool_f32_ok(H, W));
+  // the bf16 fused stem reads the f32 NCHW frames itself (no pack pass)
+  const bool direct_bf = fused && bf && direct;
+  if (!direct_bf && (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, bf, s))) return rc;
+  if (fused) {
     // fused stem conv + ReLU + maxpool (profiled as the stem layer)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) {
@@ -433,7 +440,8 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
       if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
       EOSV_HIP_CHECK(hipEventRecord(e0, s));
     }
-    if ((rc = bf ? launch_stem_pool_bf16(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s)
+    if ((rc = bf ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
+                                         direct_bf ? frames : nullptr)
                  : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s)))
       return rc;
     if (h->prof) {

@@ -24,6 +24,14 @@
 // LDS: a ring of 16 padded input rows x 4 copies (row r in slot (r + 3) & 15, so the 4 rows
 // a step prefetches are contiguous); LDS-DMA from the dense padded RGB pack (4-B aligned
 // sources).  Step py needs input rows 4py .. 4py+8 and prefetches 4py+9 .. 4py+12.
+//
+// DIRECT (default): no pack kernel.  The rows come straight from the caller's f32 NCHW frames:
+// a step LDS-DMAs the 4 rows it prefetches as 12 f32 plane rows into a staging area (issued
+// before the MFMAs), and after them a thread reads the R, G, B values of 2 padded columns from
+// the staging, rounds them to bf16 and writes the 12 interleaved bytes into all 4 shifted
+// copies (3 ds_write_b32 each); zero padding is written as zeros.  Saves the pack's 317 KB per
+// frame write + read.  (Plain per-lane global loads of the same values instead of the staging
+// DMA made the stem 45 % slower: 8-B lane stride, half-used lines.)
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -44,6 +52,8 @@ __host__ __device__ constexpr int copy_chunks(int ntiles) {
   return (12 * (14 * ntiles) + 12 + 48 + 15) / 16;
 }
 constexpr int LDS_BYTES = RING * 4 * copy_chunks(MAX_TILES) * 16;
+constexpr int STG_ROW = 256;                          // f32 per staged plane row (W <= 256)
+constexpr int STG_BYTES = 4 * 3 * STG_ROW * 4;        // DIRECT: 4 rows x 3 planes
 
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
 
@@ -62,11 +72,14 @@ __device__ __forceinline__ float row_shl(float v, int sh) {
 
 // x: padded bf16 RGB [N][H+6][Wp][3] (stem_row_pixels), w: [64][192] bf16, bias [64] f32,
 // y: [N][Hq][Wq][64] bf16 (pooled).  Grid = N images, block = 64 * ntiles threads.
+template <bool DIRECT>
 __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u16* __restrict__ x,
+                                                                       const float* __restrict__ fx,
                                                                        const u16* __restrict__ w,
                                                                        const float* __restrict__ bias, u16* y,
                                                                        int H, int W, int Hs, int Ws, int Hq, int Wq) {
-  __shared__ __attribute__((aligned(16))) unsigned char ring[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char ring[LDS_BYTES + (DIRECT ? STG_BYTES : 0)];
+  float* stg = (float*)(ring + LDS_BYTES);  // DIRECT staging: [row 4][plane 3][STG_ROW]
   const int ntiles = blockDim.x >> 6;
   const int CH = copy_chunks(ntiles);  // 16-B chunks per copy
   const int tid = threadIdx.x;
@@ -78,7 +91,60 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
   const int Wp = stem_row_pixels(W, 3);
   const int rowbytes = Wp * 6;
   const int Hpad = H + 6;
-  const unsigned char* ximg = (const unsigned char*)(x + (long long)img * Hpad * Wp * 3);
+  const unsigned char* ximg = DIRECT ? nullptr : (const unsigned char*)(x + (long long)img * Hpad * Wp * 3);
+  const float* fimg = DIRECT ? fx + (long long)img * 3 * H * W : nullptr;
+  // DIRECT: task = (padded row, column pair g); row bytes 12g .. 12g+11 = R G B of columns 2g, 2g+1
+  const int GP = Wp / 2;  // column pairs per padded row (Wp is even)
+  auto direct_load = [&](int prow, int g, float (&v)[6]) {
+    const int yy = prow - 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const float* src = fimg + (ok ? (long long)yy * W + xx : 0);  // always a valid address
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = src[(long long)c * H * W];
+        v[3 * h + c] = ok ? t : 0.f;
+      }
+    }
+  };
+  // DIRECT: 4 rows [r0, r0 + 4) x 3 planes -> staging (12 pieces of W floats, one per plane row)
+  auto stage_f32 = [&](int r0) {
+    for (int p = wid; p < 12; p += ntiles) {
+      const int rr = p / 3, c = p - 3 * (p / 3);
+      const int yy = min(max(r0 + rr - 3, 0), H - 1);  // out-of-image rows: zeroed at conversion
+      if (4 * lane < W)
+        dma16(fimg + ((long long)c * H + yy) * W + 4 * lane, stg + (rr * 3 + c) * STG_ROW);
+    }
+  };
+  auto staged_load = [&](int prow, int rr, int g, float (&v)[6]) {
+    const int yy = prow - 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const int xc = ok ? xx : 0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = stg[(rr * 3 + c) * STG_ROW + xc];
+        v[3 * h + c] = ok ? t : 0.f;
+      }
+    }
+  };
+  auto direct_store = [&](int prow, int g, const float (&v)[6]) {
+    const unsigned d0 = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    const unsigned d1 = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    const unsigned d2 = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    unsigned char* slot = ring + (size_t)(((prow + 3) & (RING - 1)) * 4) * CH * 16;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // copy m holds the row shifted by 4m bytes
+      unsigned* d = (unsigned*)(slot + (size_t)m * CH * 16 + 12 * g + 4 * m);
+      d[0] = d0;
+      d[1] = d1;
+      d[2] = d2;
+    }
+  };
 
   // weights -> registers: A fragment (j, s) = couts j*16 + r16, k = 32s + 8q .. +7
   bf16x8 wf[4][6];
@@ -157,9 +223,18 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
     }
   };
 
-  stage(0, 13);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  if constexpr (DIRECT) {
+    for (int t = tid; t < 13 * GP; t += blockDim.x) {
+      float v[6];
+      direct_load(t / GP, t % GP, v);
+      direct_store(t / GP, t % GP, v);
+    }
+    __syncthreads();
+  } else {
+    stage(0, 13);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
 
   // The pool runs on the raw accumulators: max over the window commutes with + shift, ReLU and
   // the bf16 rounding (all monotone), so only the 7 pooled values per channel get them.
@@ -172,15 +247,23 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
   const int px = 7 * wid + (r16 >> 1);  // pooled column this lane writes (even r16 <= 12)
   const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
 
+  // DIRECT: this thread's task of the 4 rows a step prefetches (4 * GP tasks <= blockDim)
+  const bool dtask = DIRECT && tid < 4 * GP;
+  const int drow = tid / GP, dg = tid - (tid / GP) * GP;
   for (int py = 0; py < Hq; ++py) {
-    if (py + 1 < Hq) stage4(4 * py + 9);
+    if constexpr (DIRECT) {
+      if (py + 1 < Hq) stage_f32(4 * py + 9);
+    } else {
+      if (py + 1 < Hq) stage4(4 * py + 9);
+    }
     f32x4 a1[4], a2[4];
     stem_row(2 * py, a1);
     stem_row(2 * py + 1, a2);
     const bool ok1 = colok && 2 * py < Hs, ok2 = colok && 2 * py + 1 < Hs;
+    unsigned pk4[4][2];  // pooled bf16 pairs, stored after the DIRECT conversion
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      unsigned pk[2];
+      unsigned(&pk)[2] = pk4[j];
 #pragma unroll
       for (int e2 = 0; e2 < 2; ++e2) {
         float o[2];
@@ -196,11 +279,30 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
         }
         pk[e2] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
       }
-      if (writer) *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk[0], pk[1]);
+      if (!DIRECT && writer)
+        *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk[0], pk[1]);
     }
-    // next step's rows have landed (their DMA is older than this step's 4 stores) and every
-    // wave is done reading the slots the step after will overwrite
-    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    if constexpr (DIRECT) {
+      // staging landed (own DMA + barrier for the other waves'; the previous step's stores are
+      // a whole step old), then convert the next step's rows into slots this step does not read
+      if (py + 1 < Hq) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (dtask) {
+          float dv[6];
+          staged_load(4 * py + 9 + drow, drow, dg, dv);
+          direct_store(4 * py + 9 + drow, dg, dv);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (writer) *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk4[j][0], pk4[j][1]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      // next step's rows have landed (their DMA is older than this step's 4 stores) and every
+      // wave is done reading the slots the step after will overwrite
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -213,14 +315,22 @@ bool stem_pool_bf16_ok(int H, int W) {
   return H >= 8 && W >= 8 && (Wq + 6) / 7 <= MAX_TILES;
 }
 
+// pack: padded bf16 RGB rows (pack_rgb_pad), or nullptr with `frames` = the f32 NCHW input
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                          hipStream_t s) {
+                          hipStream_t s, const float* frames) {
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int ntiles = (Wq + 6) / 7;
   if (ntiles > MAX_TILES || B <= 0) return B <= 0 ? EOSV_OK : (set_error("stem_pool: too wide"), EOSV_ERR_UNSUPPORTED);
-  hipLaunchKernelGGL(stem_pool_bf16_kernel, dim3(B), dim3(64 * ntiles), 0, s, (const u16*)pack, (const u16*)w, bias,
-                     (u16*)y, H, W, Hs, Ws, Hq, Wq);
+  const int Wp = stem_row_pixels(W, 3);
+  if (frames) {
+    if (4 * (Wp / 2) > 64 * ntiles) return set_error("stem_pool: direct rows need more threads"), EOSV_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(stem_pool_bf16_kernel<true>, dim3(B), dim3(64 * ntiles), 0, s, nullptr, frames, (const u16*)w,
+                       bias, (u16*)y, H, W, Hs, Ws, Hq, Wq);
+  } else {
+    hipLaunchKernelGGL(stem_pool_bf16_kernel<false>, dim3(B), dim3(64 * ntiles), 0, s, (const u16*)pack, nullptr,
+                       (const u16*)w, bias, (u16*)y, H, W, Hs, Ws, Hq, Wq);
+  }
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

@@ -165,7 +165,7 @@ static int check_bf16(int N, int H, int W, int Cin, int Cout, int k, int stride,
 
 // fused bf16 stem (7x7/2 p3, 3 -> 64) + bias + ReLU + maxpool 3x3/2 p1 vs a double reference
 // on the same bf16 operands (bf16 rounding of the stem output before the pool, as the kernel)
-static int check_stem_pool(int N, int H, int W) {
+static int check_stem_pool(int N, int H, int W, bool direct = false) {
   const int pad = 3, Wp = stem_row_pixels(W, pad), Hp = H + 2 * pad;
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs - 1) / 2 + 1, Wq = (Ws - 1) / 2 + 1;
@@ -189,7 +189,18 @@ static int check_stem_pool(int N, int H, int W) {
   hipMemcpy(dw, w.data(), w.size() * 2, hipMemcpyHostToDevice);
   hipMemcpy(db, b.data(), 64 * 4, hipMemcpyHostToDevice);
   hipMemset(dy, 0xff, ny * 2);
-  const int rc = launch_stem_pool_bf16(dx + 64, N, H, W, dw, db, dy, 0);  // 128 B front slack
+  // direct: the kernel reads f32 NCHW frames (the same values, exactly representable in bf16)
+  std::vector<float> fr((size_t)N * 3 * H * W);
+  for (int n = 0; n < N; ++n)
+    for (int i = 0; i < H; ++i)
+      for (int j = 0; j < W; ++j)
+        for (int c = 0; c < 3; ++c)
+          fr[(((size_t)n * 3 + c) * H + i) * W + j] = bf2f(x[128 / 2 + (((size_t)n * Hp + i + pad) * Wp + j + pad) * 3 + c]);
+  float* dfr;
+  hipMalloc(&dfr, fr.size() * 4);
+  hipMemcpy(dfr, fr.data(), fr.size() * 4, hipMemcpyHostToDevice);
+  const int rc = direct ? launch_stem_pool_bf16(nullptr, N, H, W, dw, db, dy, 0, dfr)
+                        : launch_stem_pool_bf16(dx + 64, N, H, W, dw, db, dy, 0);  // 128 B front slack
   hipDeviceSynchronize();
   std::vector<unsigned short> y(ny);
   hipMemcpy(y.data(), dy, ny * 2, hipMemcpyDeviceToHost);
@@ -226,8 +237,9 @@ static int check_stem_pool(int N, int H, int W) {
           maxerr = fmax(maxerr, e);
         }
   }
-  printf("%s stem_pool bf16 N%d H%d W%d rc=%d maxerr %.3e bad %ld\n", bad ? "FAIL" : "ok  ", N, H, W, rc, maxerr, bad);
-  hipFree(dx); hipFree(dw); hipFree(dy); hipFree(db);
+  printf("%s stem_pool bf16%s N%d H%d W%d rc=%d maxerr %.3e bad %ld\n", bad ? "FAIL" : "ok  ", direct ? " direct" : "",
+         N, H, W, rc, maxerr, bad);
+  hipFree(dx); hipFree(dw); hipFree(dy); hipFree(db); hipFree(dfr);
   return bad || rc ? 1 : 0;
 }
 
@@ -301,6 +313,9 @@ int main() {
   fails += check_stem_pool(2, 224, 224);
   fails += check_stem_pool(3, 100, 86);  // ragged: partial last column tile, odd pooled sizes
   fails += check_stem_pool(2, 64, 48);
+  fails += check_stem_pool(2, 224, 224, true);
+  fails += check_stem_pool(3, 100, 86, true);
+  fails += check_stem_pool(2, 64, 48, true);
   fails += check_stem_pool_f32(2, 224, 224);
   fails += check_stem_pool_f32(3, 100, 86);
   fails += check_stem_pool_f32(2, 64, 48);
