@@ -29,6 +29,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 MFMA_PEAK_TF = {"f32": 157.3, "bf16": 2516.6}  # MI355X dense peaks (MI355X_MICROARCH.md)
+# f32x3 (EOSV_F32X3): every f32-accurate product is three bf16 MFMA products, so its ceiling in
+# algorithmic (f32) FLOP/s is the bf16 dense peak / 3
+MFMA_PEAK_TF["f32x3"] = round(MFMA_PEAK_TF["bf16"] / 3, 1)
+ELEM_BYTES = {"f32": 4, "bf16": 2, "f32x3": 6}  # activation bytes per element (f32x3: hi, lo, hi)
 
 
 def parse():
@@ -51,8 +55,10 @@ def parse():
     ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
     ap.add_argument("--config-label", default="BASELINE configs[1]",
                     help="which BASELINE.json config this run measures (tools/bench_configs.py sets it)")
-    ap.add_argument("--secondary-dtype", default="bf16",
-                    help="also time the same episodes with this backbone dtype ('' to skip)")
+    ap.add_argument("--secondary-dtype", default="bf16,f32x3",
+                    help="also time the same episodes with these backbone dtypes, comma-separated "
+                         "('' or none to skip); the first is reported as 'secondary', the others as "
+                         "'secondary_<dtype>'")
     return ap.parse_args()
 
 
@@ -96,7 +102,8 @@ def cpu_baseline(args, episodes, T):
 
 
 def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
-    """Warmup + timed region for one backbone dtype; returns (elapsed_s, preds, per-layer profile)."""
+    """Warmup + timed region for one backbone dtype; returns (elapsed_s, preds, per-layer profile,
+    clip embeddings of the last step)."""
     bb = engine.Backbone(args.arch, dtype, args.res, args.res, max_frames=args.max_frames, device=local)
     bb.load_state_dict(synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
     feat = torch.empty(max(d.batch.n_frames for d in batches), bb.D, device=f"cuda:{local}")
@@ -112,7 +119,7 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     t0 = time.perf_counter()
     for s in range(args.warmup, len(batches)):
         d = batches[s]
-        p, _, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
+        p, emb, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
         preds.append(p)
     torch.cuda.synchronize()
     if dist:
@@ -123,7 +130,7 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     bb.profile(False)
     bb.close()
     from eosv import dist as edist
-    return edist.max_over_ranks(elapsed), torch.cat(preds), prof
+    return edist.max_over_ranks(elapsed), torch.cat(preds), prof, emb.cpu().numpy()
 
 
 def measured_traffic(dtype, key):
@@ -146,9 +153,9 @@ def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches, chunks
     """Conv-family algorithmic bytes per launch: every layer's input + output (+ residual) map
     once per frame and its weights once per chunk (arch.conv_layer_bytes: the unfused plan's
     floor; with the downsample folded into the block's last conv there are fewer launches)."""
-    elem = 2 if dtype == "bf16" else 4
+    elem = ELEM_BYTES[dtype]
     layers = arch_mod.conv_layer_bytes(arch_mod.SPECS[args.arch], args.res, args.res, elem,
-                                       stem_pool_fused=(dtype == "bf16"))
+                                       stem_pool_fused=(dtype != "f32"))
     per_frame = sum(b for b, _ in layers)
     weights = sum(w for _, w in layers)
     return (frames * per_frame + chunks * weights) / launches
@@ -163,6 +170,9 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
            "frac": round(achieved / peak, 4), "traffic": None,
            "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
                      f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
+    if dtype == "f32x3":
+        out["kernel"] += ("; f32x3 = conv_bf16 kernels on the split (hi, lo, hi) layout + the exact-f32 "
+                          "stem, algorithmic (f32) FLOPs; peak = bf16 dense peak / 3")
     if args is not None and nl.sum() > 0:
         tr, src = measured_traffic(dtype, f"{args.arch}@{args.res}x{args.res}")
         out["traffic"] = tr
@@ -198,7 +208,7 @@ def main():
     torch.cuda.synchronize()
     timed_idx = mine_idx[args.warmup * E:]
 
-    elapsed, pred, prof = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
+    elapsed, pred, prof, emb = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
     clips = edist.sum_over_ranks(sum(d.batch.n_clips for d in batches[args.warmup:]))
     frames_rank = sum(d.batch.n_frames for d in batches[args.warmup:])
     frames = edist.sum_over_ranks(frames_rank)
@@ -208,15 +218,19 @@ def main():
     qy = np.array([p["query_y"] for p in plans])
     acc = float((preds[timed] == qy[timed]).mean())
 
-    secondary = None
-    if args.secondary_dtype and args.secondary_dtype not in ("none", args.dtype):
-        el2, pred2, prof2 = run_timed(args, engine, arch_mod, synth, batches, args.secondary_dtype, local, dist)
+    legs = []
+    for dt2 in [d for d in (args.secondary_dtype or "").split(",") if d and d not in ("none", args.dtype)]:
+        el2, pred2, prof2, emb2 = run_timed(args, engine, arch_mod, synth, batches, dt2, local, dist)
+        # clip embeddings of the last step vs the f32 primary: max over clips of
+        # max|e - e_f32| / max|e_f32| (the north star's 1e-4 relative bound, tests/test_gpu_parity.py)
+        emb_rel = float((np.abs(emb2 - emb).max(1) / np.maximum(np.abs(emb).max(1), 1e-30)).max())
         preds2 = edist.gather_predictions(timed_idx, pred2.cpu().numpy(), len(plans))
-        secondary = {"dtype": args.secondary_dtype, "value": round(clips / el2, 2), "unit": "clips/s",
+        legs.append({"dtype": dt2, "value": round(clips / el2, 2), "unit": "clips/s",
                      "ms_per_step": round(el2 / args.steps * 1e3, 3),
                      "prediction_agreement_vs_primary": round(float((preds2[timed] == preds[timed]).mean()), 4),
                      "episode_acc": round(float((preds2[timed] == qy[timed]).mean()), 4),
-                     "roofline": roofline(prof2, args.secondary_dtype, args, arch_mod, frames_rank)}
+                     "embedding_max_rel_vs_primary": float(f"{emb_rel:.3g}"),
+                     "roofline": roofline(prof2, dt2, args, arch_mod, frames_rank)})
 
     if rank == 0:
         ms, fl, nl = prof
@@ -248,8 +262,8 @@ def main():
             "roofline": rl,
             "cpu_baseline": None,
         }
-        if secondary:
-            out["secondary"] = secondary
+        for i, leg in enumerate(legs):
+            out["secondary" if i == 0 else "secondary_" + leg["dtype"]] = leg
         if args.layers:
             for i in range(len(ms)):
                 if nl[i]:

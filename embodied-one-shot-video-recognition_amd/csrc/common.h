@@ -50,6 +50,10 @@ struct ConvArgs {
   // (oh, ow) -> x2 pixel (oh * stride2, ow * stride2), channel k - K1; nullptr = none
   const void* x2;     // NHWC [N, H2, W2, Cin2]
   int H2, W2, Cin2, stride2, K1;
+  // bf16 kernels, EOSV_F32X3: activations are [pixel][3 * C] bf16 = (hi, lo, hi) blocks of C
+  // channels; Cin / Cin2 / K count those 3C virtual input channels (weights (w_hi, w_hi, w_lo)),
+  // Cout is the logical C.  The epilogue reads the residual as hi + lo and stores hi, lo, hi.
+  int split;
 };
 
 // Workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one L2;
@@ -71,7 +75,7 @@ int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, 
                           hipStream_t s, const float* frames = nullptr);
 bool stem_pool_f32_ok(int H, int W);  // stem_pool_f32.hip: the same for f32
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                         hipStream_t s);
+                         hipStream_t s, bool split = false);  // split: y in the EOSV_F32X3 (hi, lo, hi) layout
 bool conv_bf16_p8_ok(const ConvArgs& a);  // conv_bf16_p8.hip: phased 8-wave implicit GEMM
 bool conv_bf16_p8_default(const ConvArgs& a);
 int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s);
@@ -88,6 +92,7 @@ inline size_t stem_input_elems(int B, int H, int W, int pad) {
 int launch_pack_rgb_pad(const float* x, int B, int H, int W, int pad, void* y, int bf16, hipStream_t s);
 int launch_maxpool3x3s2(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo,
                         int bf16, hipStream_t s);
+// bf16: 0 f32 input, 1 bf16, 2 the EOSV_F32X3 split layout (value = hi + lo)
 int launch_avgpool(const void* x, int B, int HW, int C, float* y, int bf16, hipStream_t s);
 
 }  // namespace eosv

@@ -29,7 +29,8 @@ __device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__
 
 // MF = MFMA tile edge: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16; same
 // cycles per FLOP, but the chip holds a higher clock on it with random operands)
-template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS>
+// SPLIT: EOSV_F32X3 epilogue (ConvArgs::split): residual = hi + lo, output stored as (hi, lo, hi)
+template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BK = 64;  // bf16 elements per row = 128 B
   constexpr int NW = WM * WN;
@@ -240,27 +241,32 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // residual chunks of pass i, loaded one pass ahead (pass 0's right after the K-loop) so
   // their latency overlaps the LDS staging instead of stalling each store
   uint4 rv[2][IPT];
+  uint4 rl[2][SPLIT ? IPT : 1];  // SPLIT: the residual's lo block
+  const long long ostr = SPLIT ? 3LL * a.Cout : a.Cout;  // output / residual pixel stride
   auto chunk = [&](int i, int t, int& lrow, int& c8, long long& o) {
     const int idx = tid + t * nthreads;
     lrow = idx / (BN / 8);
     c8 = idx - lrow * (BN / 8);
     const int m = m0 + (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
     const int n = n0 + c8 * 8;
-    o = (m < M && n < a.Cout) ? (long long)m * a.Cout + n : -1;
+    o = (m < M && n < a.Cout) ? (long long)m * ostr + n : -1;
   };
-  auto load_res = [&](int i, uint4 (&r4)[IPT]) {
+  auto load_res = [&](int i) {
 #pragma unroll
     for (int t = 0; t < IPT; ++t) {
       int lrow, c8;
       long long o;
       chunk(i, t, lrow, c8, o);
-      if (o >= 0) r4[t] = *(const uint4*)(res + o);
+      if (o >= 0) {
+        rv[i & 1][t] = *(const uint4*)(res + o);
+        if constexpr (SPLIT) rl[i & 1][SPLIT ? t : 0] = *(const uint4*)(res + o + a.Cout);
+      }
     }
   };
-  if (res) load_res(0, rv[0]);
+  if (res) load_res(0);
 #pragma unroll
   for (int i = 0; i < NPASS; ++i) {
-    if (res && i + 1 < NPASS) load_res(i + 1, rv[(i + 1) & 1]);
+    if (res && i + 1 < NPASS) load_res(i + 1);
     // raw barriers in the epilogue: only the LDS staging needs ordering, and a
     // __syncthreads() fence would also wait for the residual prefetch and the stores
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -290,13 +296,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
       if (res) {
         const uint4 r4 = rv[i & 1][t];
         const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
+        if constexpr (SPLIT) {
+          const uint4 l4 = rl[i & 1][SPLIT ? t : 0];
+          const unsigned rlo[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff));
-          v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16));
+          for (int k = 0; k < 4; ++k) {  // hi + lo is exact in f32
+            v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff)) + bf_to_f((u16)(rlo[k] & 0xffff));
+            v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16)) + bf_to_f((u16)(rlo[k] >> 16));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff));
+            v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16));
+          }
         }
       }
-      unsigned pk[4];
+      unsigned pk[4], pl[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float lo = v[2 * k], hi = v[2 * k + 1];
@@ -304,12 +320,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
           lo = fmaxf(lo, 0.f);
           hi = fmaxf(hi, 0.f);
         }
-        pk[k] = (unsigned)f_to_bf(lo) | ((unsigned)f_to_bf(hi) << 16);
+        const u16 blo = f_to_bf(lo), bhi = f_to_bf(hi);
+        pk[k] = (unsigned)blo | ((unsigned)bhi << 16);
+        if constexpr (SPLIT)  // residual parts (exact differences)
+          pl[k] = (unsigned)f_to_bf(lo - bf_to_f(blo)) | ((unsigned)f_to_bf(hi - bf_to_f(bhi)) << 16);
       }
-      if (a.abl & 2)
+      if (a.abl & 2) {
         asm volatile("" ::"v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]));
-      else
+      } else {
         *(uint4*)(y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        if constexpr (SPLIT) {
+          *(uint4*)(y + o + a.Cout) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
+          *(uint4*)(y + o + 2 * a.Cout) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
+      }
     }
   }
 }
@@ -335,7 +359,16 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
-  if (a.x2) {
+  if (a.split) {
+    if (STEM || (a.x2 && (a.K1 % 64 || a.Cin2 % 64)))
+      return set_error("conv_bf16: split layout shape"), EOSV_ERR_UNSUPPORTED;
+    if (a.x2)
+      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, true>), dim3((unsigned)nb),
+                         dim3(64 * WM * WN), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, true>), dim3((unsigned)nb),
+                         dim3(64 * WM * WN), 0, s, a);
+  } else if (a.x2) {
     if (STEM || a.K1 % 64 || a.Cin2 % 64) return set_error("conv_bf16: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
     hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
                        s, a);
@@ -380,7 +413,7 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
-  if (bf16_rows() && !a.x2 && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
   if (bf16_p8() && conv_bf16_p8_ok(a) && (bf16_p8() == 2 || conv_bf16_p8_default(a))) return launch_conv_bf16_p8(a, s);
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
   // K = 64 1x1 convs all measured slower than this choice

@@ -36,7 +36,8 @@ __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
 }  // namespace
 
-template <int BM, int BN, int WM, int WN, bool DS>
+// SPLIT: EOSV_F32X3 epilogue (ConvArgs::split), as in conv_bf16.hip
+template <int BM, int BN, int WM, int WN, bool DS, bool SPLIT = false>
 __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
   constexpr int BK = 64;
   constexpr int NW = 8;
@@ -291,27 +292,32 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
   constexpr int IPT = EPR * (BN / 8) / (64 * NW);  // 16-B output chunks per thread per pass
   static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
   uint4 rv[2][IPT];
+  uint4 rl[2][SPLIT ? IPT : 1];  // SPLIT: the residual's lo block
+  const long long ostr = SPLIT ? 3LL * a.Cout : a.Cout;  // output / residual pixel stride
   auto chunk = [&](int i, int t, int& lrow, int& c8, long long& o) {
     const int idx = tid + t * 64 * NW;
     lrow = idx / (BN / 8);
     c8 = idx - lrow * (BN / 8);
     const int m = m0 + (lrow >> 5) * 128 + i * 32 + (lrow & 31);
     const int n = n0 + c8 * 8;
-    o = (m < M && n < a.Cout) ? (long long)m * a.Cout + n : -1;
+    o = (m < M && n < a.Cout) ? (long long)m * ostr + n : -1;
   };
-  auto load_res = [&](int i, uint4 (&r4)[IPT]) {
+  auto load_res = [&](int i) {
 #pragma unroll
     for (int t = 0; t < IPT; ++t) {
       int lrow, c8;
       long long o;
       chunk(i, t, lrow, c8, o);
-      if (o >= 0) r4[t] = *(const uint4*)(res + o);
+      if (o >= 0) {
+        rv[i & 1][t] = *(const uint4*)(res + o);
+        if constexpr (SPLIT) rl[i & 1][SPLIT ? t : 0] = *(const uint4*)(res + o + a.Cout);
+      }
     }
   };
-  if (res) load_res(0, rv[0]);
+  if (res) load_res(0);
 #pragma unroll
   for (int i = 0; i < NPASS; ++i) {
-    if (res && i + 1 < NPASS) load_res(i + 1, rv[(i + 1) & 1]);
+    if (res && i + 1 < NPASS) load_res(i + 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -338,13 +344,23 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
       if (res) {
         const uint4 r4 = rv[i & 1][t];
         const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
+        if constexpr (SPLIT) {
+          const uint4 l4 = rl[i & 1][SPLIT ? t : 0];
+          const unsigned rlo[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[2 * k] += bf2f((u16)(ru[k] & 0xffff));
-          v[2 * k + 1] += bf2f((u16)(ru[k] >> 16));
+          for (int k = 0; k < 4; ++k) {  // hi + lo is exact in f32
+            v[2 * k] += bf2f((u16)(ru[k] & 0xffff)) + bf2f((u16)(rlo[k] & 0xffff));
+            v[2 * k + 1] += bf2f((u16)(ru[k] >> 16)) + bf2f((u16)(rlo[k] >> 16));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] += bf2f((u16)(ru[k] & 0xffff));
+            v[2 * k + 1] += bf2f((u16)(ru[k] >> 16));
+          }
         }
       }
-      unsigned pk[4];
+      unsigned pk[4], pl[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float lo = v[2 * k], hi = v[2 * k + 1];
@@ -352,12 +368,20 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
           lo = fmaxf(lo, 0.f);
           hi = fmaxf(hi, 0.f);
         }
-        pk[k] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+        const u16 blo = f2bf(lo), bhi = f2bf(hi);
+        pk[k] = (unsigned)blo | ((unsigned)bhi << 16);
+        if constexpr (SPLIT)  // residual parts (exact differences)
+          pl[k] = (unsigned)f2bf(lo - bf2f(blo)) | ((unsigned)f2bf(hi - bf2f(bhi)) << 16);
       }
-      if (a.abl & 2)
+      if (a.abl & 2) {
         asm volatile("" ::"v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]));
-      else
+      } else {
         *(uint4*)(y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        if constexpr (SPLIT) {
+          *(uint4*)(y + o + a.Cout) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
+          *(uint4*)(y + o + 2 * a.Cout) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
+      }
     }
   }
 }
@@ -380,7 +404,19 @@ int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s) {
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv_bf16_p8: grid too large"), EOSV_ERR_UNSUPPORTED;
   if (a.x2 && (a.K1 % 64 || a.Cin2 % 64)) return set_error("conv_bf16_p8: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
-  if (a.Cout == 128) {
+  if (a.split) {
+#define P8_SPLIT(BM_, BN_, WM_, WN_)                                                                          \
+  if (a.x2)                                                                                                 \
+    hipLaunchKernelGGL((conv_bf16_p8_kernel<BM_, BN_, WM_, WN_, true, true>), dim3((unsigned)nb), dim3(512), 0, s, a); \
+  else                                                                                                      \
+    hipLaunchKernelGGL((conv_bf16_p8_kernel<BM_, BN_, WM_, WN_, false, true>), dim3((unsigned)nb), dim3(512), 0, s, a);
+    if (a.Cout == 128) {
+      P8_SPLIT(512, 128, 4, 2)
+    } else {
+      P8_SPLIT(256, 256, 2, 4)
+    }
+#undef P8_SPLIT
+  } else if (a.Cout == 128) {
     if (a.x2)
       hipLaunchKernelGGL((conv_bf16_p8_kernel<512, 128, 4, 2, true>), dim3((unsigned)nb), dim3(512), 0, s, a);
     else

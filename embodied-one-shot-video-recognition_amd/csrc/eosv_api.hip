@@ -76,6 +76,14 @@ namespace eosv {
 
 static int conv_out(int h, int k, int s, int p) { return (h + 2 * p - k) / s + 1; }
 
+// dtype roles: the residual-block convs run on the bf16 kernels for EOSV_BF16 and EOSV_F32X3;
+// the stem is bf16 only for EOSV_BF16 (EOSV_F32X3 keeps it exact f32, split output)
+static bool x3(const eosv_handle* h) { return h->d.dtype == EOSV_F32X3; }
+static bool conv_bf(const eosv_handle* h) { return h->d.dtype != EOSV_F32; }
+static bool stem_bf(const eosv_handle* h) { return h->d.dtype == EOSV_BF16; }
+// bytes per activation element: f32 4, bf16 2, split (hi, lo, hi) 6
+static size_t act_bytes(const eosv_handle* h) { return x3(h) ? 6 : conv_bf(h) ? 2 : 4; }
+
 static Conv make_conv(int cin, int cout, int k, int stride, int pad, const std::string& wname,
                       const std::string& bnname) {
   Conv c;
@@ -189,6 +197,20 @@ static int build_plan(eosv_handle* h) {
   }
   h->fc.id = id++;
   h->n_layers = id;
+  if (x3(h)) {
+    // split layout: every block conv reads 3 * cin virtual channels (hi, lo, hi)
+    auto widen = [](Conv& c) {
+      c.cinp = 3 * c.cin;
+      c.K = c.kh * c.kw * c.cinp;
+      c.kds *= 3;
+    };
+    for (Block& b : h->blocks) {
+      widen(b.c1);
+      widen(b.c2);
+      if (b.bottleneck) widen(b.c3);
+      if (b.has_ds) widen(b.ds);
+    }
+  }
   return EOSV_OK;
 }
 
@@ -231,8 +253,18 @@ struct Tensors {
 
 // fold BN (eval) into the conv: host [cout][K] weights (K order as the kernels read it) and
 // [cout] shift.  False (error set) on a missing tensor.
+static float bf_round_host(float f) {
+  const unsigned u = (unsigned)f2bf_host(f) << 16;
+  float r;
+  memcpy(&r, &u, 4);
+  return r;
+}
+
+// split (EOSV_F32X3): c.cinp = 3 * c.cin virtual input channels; folded weight v goes to
+// channels i and cin + i as hi = bf16(v) and to 2 cin + i as lo = bf16(v - hi), so the
+// (hi, lo, hi) activation blocks give hi.hi + lo.hi + hi.lo
 static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::vector<float>& wf,
-                      std::vector<float>& beta) {
+                      std::vector<float>& beta, bool split = false) {
   const float* w = t.get(c.wname, (int64_t)c.cout * c.cin * c.kh * c.kw);
   if (!w) return false;
   std::vector<float> alpha(c.cout, 1.f);
@@ -258,26 +290,38 @@ static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::ve
   // (conv_bf16_p8.hip)
   c.kcm = bf16 && !c.stem && c.cinp % 64 == 0 && c.cinp > 64 && c.kh * c.kw > 1 && c.kwp == c.kw;
   wf.assign((size_t)c.cout * c.K, 0.f);
+  if (split && c.cinp != 3 * c.cin) return set_error("fold_conv: split layout needs 3 * cin channels"), false;
+  auto kidx = [&](int i, int y, int x) {
+    return c.kcm ? ((size_t)(i / 64) * c.kh * c.kw + y * c.kw + x) * 64 + i % 64
+                 : ((size_t)y * c.kwp + x) * c.cinp + i;
+  };
   for (int o = 0; o < c.cout; ++o)
     for (int i = 0; i < c.cin; ++i)
       for (int y = 0; y < c.kh; ++y)
         for (int x = 0; x < c.kw; ++x) {
-          const float v = w[(((size_t)o * c.cin + i) * c.kh + y) * c.kw + x];
-          const size_t k = c.kcm ? ((size_t)(i / 64) * c.kh * c.kw + y * c.kw + x) * 64 + i % 64
-                                 : ((size_t)y * c.kwp + x) * c.cinp + i;
-          wf[(size_t)o * c.K + k] = v * alpha[o];
+          const float v = w[(((size_t)o * c.cin + i) * c.kh + y) * c.kw + x] * alpha[o];
+          float* row = wf.data() + (size_t)o * c.K;
+          if (!split) {
+            row[kidx(i, y, x)] = v;
+          } else {
+            const float hi = bf_round_host(v);
+            row[kidx(i, y, x)] = hi;
+            row[kidx(c.cin + i, y, x)] = hi;
+            row[kidx(2 * c.cin + i, y, x)] = bf_round_host(v - hi);
+          }
         }
   return true;
 }
 
 // upload [cout][K (+ ds K)] weights + [cout] bias; with `ds`, the downsample's folded 1x1
 // weights are appended as K columns [c.K, c.K + ds.cin) and its shift is added to the bias
-static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, bool has_bn, Conv* ds = nullptr) {
+static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, bool has_bn, Conv* ds = nullptr,
+                       bool split = false) {
   std::vector<float> wf, beta;
-  if (!fold_conv(c, t, bf16, has_bn, wf, beta)) return EOSV_ERR_ARG;
+  if (!fold_conv(c, t, bf16, has_bn, wf, beta, split)) return EOSV_ERR_ARG;
   if (ds) {
     std::vector<float> wd, bd;
-    if (!fold_conv(*ds, t, bf16, true, wd, bd)) return EOSV_ERR_ARG;
+    if (!fold_conv(*ds, t, bf16, true, wd, bd, split)) return EOSV_ERR_ARG;
     if (ds->cout != c.cout || ds->kh != 1 || ds->K != c.kds) return set_error("fused downsample shape"), EOSV_ERR_ARG;
     const int Kt = c.K + c.kds;
     std::vector<float> wc((size_t)c.cout * Kt);
@@ -350,6 +394,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   }();
   a.xcd = xcd;
   a.kcm = c.kcm ? 1 : 0;
+  a.split = (bf16 && x3(h)) ? 1 : 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);
@@ -360,7 +405,8 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   const int rc = bf16 ? launch_conv_bf16(a, s) : launch_conv_f32(a, s);
   if (h->prof && rc == EOSV_OK) {
     EOSV_HIP_CHECK(hipEventRecord(e1, s));
-    const double macs = (double)N * a.Ho * a.Wo * c.cout * ((double)c.kh * c.kw * c.cin + (x2 ? c.kds : 0));
+    // algorithmic MACs: logical channels (the split layout's 3x virtual K is not counted)
+    const double macs = (double)N * a.Ho * a.Wo * c.cout * ((double)c.kh * c.kw * c.cin + (x2 ? c.kds / (a.split ? 3 : 1) : 0));
     h->recs.push_back({c.id, e0, e1, 2.0 * macs});
   }
   return rc;
@@ -427,10 +473,12 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
     const char* e = getenv("EOSV_STEM_DIRECT");  // 0 = pack kernel + LDS-DMA rows (A/B switch)
     return !e || atoi(e) != 0;
   }();
-  const bool fused = stem_pool_fused(bf) && (bf ? stem_pool_bf16_ok(H, W) : stem_pool_f32_ok(H, W));
+  const bool sbf = stem_bf(h);  // EOSV_F32X3: exact-f32 stem with split output, bf16 blocks
+  const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W) : stem_pool_f32_ok(H, W));
+  if (x3(h) && !fused) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
   // the bf16 fused stem reads the f32 NCHW frames itself (no pack pass)
-  const bool direct_bf = fused && bf && direct;
-  if (!direct_bf && (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, bf, s))) return rc;
+  const bool direct_bf = fused && sbf && direct;
+  if (!direct_bf && (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s))) return rc;
   if (fused) {
     // fused stem conv + ReLU + maxpool (profiled as the stem layer)
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -440,9 +488,9 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
       if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
       EOSV_HIP_CHECK(hipEventRecord(e0, s));
     }
-    if ((rc = bf ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
-                                         direct_bf ? frames : nullptr)
-                 : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s)))
+    if ((rc = sbf ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
+                                          direct_bf ? frames : nullptr)
+                  : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s, x3(h))))
       return rc;
     if (h->prof) {
       EOSV_HIP_CHECK(hipEventRecord(e1, s));
@@ -457,8 +505,8 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
 }
 
 static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat, hipStream_t s) {
-  const bool bf = h->d.dtype == EOSV_BF16;
-  const size_t elt = bf ? 2 : 4;
+  const bool bf = conv_bf(h);
+  const size_t elt = act_bytes(h);
   int rc;
   void* x;
   int hh = h->hp, ww = h->wp;
@@ -479,7 +527,7 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
   hh = h->front_hw[0];
   ww = h->front_hw[1];
   if ((rc = run_blocks(h, h->n_front, h->blocks.size(), x, h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
-  return launch_avgpool(x, B, hh * ww, h->D, feat, bf, s);
+  return launch_avgpool(x, B, hh * ww, h->D, feat, x3(h) ? 2 : bf ? 1 : 0, s);
 }
 
 }  // namespace eosv
@@ -497,18 +545,18 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   }
   *out = nullptr;
   if (desc->height < 32 || desc->width < 32 || desc->max_frames <= 0 || desc->num_classes <= 0 ||
-      (desc->dtype != EOSV_F32 && desc->dtype != EOSV_BF16)) {
-    set_error("eosv_create: bad desc (height/width >= 32, max_frames > 0, dtype f32|bf16)");
+      (desc->dtype != EOSV_F32 && desc->dtype != EOSV_BF16 && desc->dtype != EOSV_F32X3)) {
+    set_error("eosv_create: bad desc (height/width >= 32, max_frames > 0, dtype f32|bf16|f32x3)");
     return EOSV_ERR_ARG;
   }
   EOSV_HIP_CHECK(hipSetDevice(desc->device));
   eosv_handle* h = new eosv_handle();
   h->d = *desc;
   int rc = build_plan(h);
-  const size_t elt = desc->dtype == EOSV_BF16 ? 2 : 4;
+  const size_t elt = act_bytes(h);
   const size_t F = (size_t)desc->max_frames;
   // + 256 B: the fused bf16 stem's DMA reads up to 12 B before a row (stem_pool_bf16.hip)
-  const size_t pack_bytes = stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * elt + 256;
+  const size_t pack_bytes = stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * (stem_bf(h) ? 2 : 4) + 256;
   void* pack_base = nullptr;
   if (!rc) rc = dmalloc(h, &pack_base, pack_bytes);
   // zero borders of the padded stem input: written once here, the packer only fills interiors
@@ -546,16 +594,16 @@ int eosv_load_weights(eosv_handle* h, const char* const* names, const void* cons
     if (!names[i]) continue;
     t.m[names[i]] = {(const float*)host_ptrs[i], numel[i]};
   }
-  const bool bf = h->d.dtype == EOSV_BF16;
+  const bool bf = conv_bf(h), sp = x3(h);
   int rc;
   h->loaded = false;
-  if ((rc = upload_conv(h, h->stem, t, bf, true))) return rc;
+  if ((rc = upload_conv(h, h->stem, t, stem_bf(h), true))) return rc;
   for (Block& b : h->blocks) {
-    if ((rc = upload_conv(h, b.c1, t, bf, true))) return rc;
+    if ((rc = upload_conv(h, b.c1, t, bf, true, nullptr, sp))) return rc;
     Conv* fds = b.fuse_ds ? &b.ds : nullptr;
-    if ((rc = upload_conv(h, b.c2, t, bf, true, b.bottleneck ? nullptr : fds))) return rc;
-    if (b.bottleneck && (rc = upload_conv(h, b.c3, t, bf, true, fds))) return rc;
-    if (b.has_ds && !b.fuse_ds && (rc = upload_conv(h, b.ds, t, bf, true))) return rc;
+    if ((rc = upload_conv(h, b.c2, t, bf, true, b.bottleneck ? nullptr : fds, sp))) return rc;
+    if (b.bottleneck && (rc = upload_conv(h, b.c3, t, bf, true, fds, sp))) return rc;
+    if (b.has_ds && !b.fuse_ds && (rc = upload_conv(h, b.ds, t, bf, true, nullptr, sp))) return rc;
   }
   Conv& fc = h->fc;
   fc.bnname = "fc.bias";

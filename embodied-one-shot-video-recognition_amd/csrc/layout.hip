@@ -137,14 +137,18 @@ int launch_maxpool3x3s2(const void* x, int B, int H, int W, int C, void* y, int 
 }
 
 // one thread = one (frame, channel); consecutive threads = consecutive channels (coalesced)
-template <bool BF16>
+template <bool BF16, bool SPLIT = false>
 __global__ void avgpool_kernel(const void* __restrict__ xv, int B, int HW, int C, float* __restrict__ y) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)B * C) return;
   const long long b = t / C;
   const int c = (int)(t - b * C);
   float s = 0.f;
-  if constexpr (BF16) {
+  if constexpr (SPLIT) {
+    // EOSV_F32X3 layout [pixel][hi C | lo C | hi C]: value = hi + lo (exact in f32)
+    const unsigned short* x = (const unsigned short*)xv + b * HW * 3 * C + c;
+    for (int p = 0; p < HW; ++p) s += bf2f(x[(long long)p * 3 * C]) + bf2f(x[(long long)p * 3 * C + C]);
+  } else if constexpr (BF16) {
     const unsigned short* x = (const unsigned short*)xv + b * HW * C + c;
     for (int p = 0; p < HW; ++p) s += bf2f(x[(long long)p * C]);
   } else {
@@ -157,7 +161,9 @@ __global__ void avgpool_kernel(const void* __restrict__ xv, int B, int HW, int C
 int launch_avgpool(const void* x, int B, int HW, int C, float* y, int bf16, hipStream_t s) {
   const long long total = (long long)B * C;
   const unsigned grid = (unsigned)((total + 255) / 256);
-  if (bf16)
+  if (bf16 == 2)
+    hipLaunchKernelGGL((avgpool_kernel<true, true>), dim3(grid), dim3(256), 0, s, x, B, HW, C, y);
+  else if (bf16)
     hipLaunchKernelGGL(avgpool_kernel<true>, dim3(grid), dim3(256), 0, s, x, B, HW, C, y);
   else
     hipLaunchKernelGGL(avgpool_kernel<false>, dim3(grid), dim3(256), 0, s, x, B, HW, C, y);

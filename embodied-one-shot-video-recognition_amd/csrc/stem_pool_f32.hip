@@ -23,6 +23,8 @@
 // 4py .. 4py+8 and prefetches 4py+9 .. 4py+12), each row Wp * 3 floats padded to 16 B,
 // filled by LDS-DMA from the dense padded RGB pack (8-B aligned sources).  ~80 KiB: two
 // workgroups (16 waves) per CU.
+#include <hip/hip_bf16.h>
+
 #include "common.h"
 
 namespace eosv {
@@ -54,9 +56,11 @@ __device__ __forceinline__ float row_shl(float v, int sh) {
 
 // x: padded f32 RGB [N][H+6][Wp][3] (stem_row_pixels), w: [64][176] f32, bias [64] f32,
 // y: [N][Hq][Wq][64] f32 (pooled).  Grid = N images, block = 64 * ntiles threads.
+// SPLIT (EOSV_F32X3): y is [N][Hq][Wq][192] bf16, (hi, lo, hi) of each pooled f32 value.
+template <bool SPLIT>
 __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                              const float* __restrict__ w,
-                                                                             const float* __restrict__ bias, float* y,
+                                                                             const float* __restrict__ bias, void* y,
                                                                              int H, int W, int Hs, int Ws, int Hq,
                                                                              int Wq) {
   extern __shared__ __attribute__((aligned(16))) float spf_smem[];
@@ -130,7 +134,8 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
   f32x4 prev[4];  // stem row 2py - 1
 #pragma unroll
   for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
-  float* yimg = y + (long long)img * Hq * Wq * 64;
+  float* yimg = (float*)y + (long long)img * Hq * Wq * 64;
+  unsigned short* ysp = (unsigned short*)y + (long long)img * Hq * Wq * 192;
   const int px = 7 * wid + (r16 >> 1);  // pooled column this lane writes (even r16 <= 12)
   const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
 
@@ -152,7 +157,26 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
         const float c = fmaxf(fmaxf(v, row_shl(v, 1)), row_shl(v, 2));
         o[e] = fmaxf(c + bv[j][e], 0.f);
       }
-      if (writer) *(float4*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
+      if (!writer) continue;
+      if constexpr (SPLIT) {
+        unsigned hi[2], lo[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const unsigned short h0 = __bfloat16_as_ushort(__float2bfloat16(o[2 * h]));
+          const unsigned short h1 = __bfloat16_as_ushort(__float2bfloat16(o[2 * h + 1]));
+          const float r0 = o[2 * h] - __uint_as_float((unsigned)h0 << 16);  // exact
+          const float r1 = o[2 * h + 1] - __uint_as_float((unsigned)h1 << 16);
+          hi[h] = (unsigned)h0 | ((unsigned)h1 << 16);
+          lo[h] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(r0)) |
+                  ((unsigned)__bfloat16_as_ushort(__float2bfloat16(r1)) << 16);
+        }
+        unsigned short* d = ysp + ((long long)py * Wq + px) * 192 + j * 16 + 4 * q;
+        *(uint2*)d = make_uint2(hi[0], hi[1]);
+        *(uint2*)(d + 64) = make_uint2(lo[0], lo[1]);
+        *(uint2*)(d + 128) = make_uint2(hi[0], hi[1]);
+      } else {
+        *(float4*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
+      }
     }
     // next step's rows have landed (their DMA is older than this step's 4 stores) and every
     // wave is done reading the slots the step after will overwrite
@@ -169,7 +193,7 @@ bool stem_pool_f32_ok(int H, int W) {
 }
 
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                         hipStream_t s) {
+                         hipStream_t s, bool split) {
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int ntiles = (Wq + 6) / 7;
@@ -177,8 +201,12 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
   if (ntiles > SPF_MAX_TILES) return set_error("stem_pool_f32: too wide"), EOSV_ERR_UNSUPPORTED;
   const size_t lds = (size_t)(SPF_W_FLOATS + SPF_RING * spf_row_floats(stem_row_pixels(W, 3))) * 4;
   if (lds > 163840) return set_error("stem_pool_f32: rows too wide for LDS"), EOSV_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(stem_pool_f32_kernel, dim3(B), dim3(64 * ntiles), lds, s, (const float*)pack, (const float*)w,
-                     bias, (float*)y, H, W, Hs, Ws, Hq, Wq);
+  if (split)
+    hipLaunchKernelGGL(stem_pool_f32_kernel<true>, dim3(B), dim3(64 * ntiles), lds, s, (const float*)pack,
+                       (const float*)w, bias, y, H, W, Hs, Ws, Hq, Wq);
+  else
+    hipLaunchKernelGGL(stem_pool_f32_kernel<false>, dim3(B), dim3(64 * ntiles), lds, s, (const float*)pack,
+                       (const float*)w, bias, y, H, W, Hs, Ws, Hq, Wq);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

@@ -12,7 +12,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "libeosv.so")
 
-EOSV_F32, EOSV_BF16 = 0, 1
+EOSV_F32, EOSV_BF16, EOSV_F32X3 = 0, 1, 2
 MATCH_PROTONET, MATCH_COSINE = 0, 1
 MAX_COLS = 64
 

@@ -22,11 +22,12 @@ import numpy as np
 import torch
 
 from . import synth
-from ._lib import (EOSV_BF16, EOSV_F32, MATCH_COSINE, MATCH_PROTONET, MAX_COLS, EosvDesc, check,
+from ._lib import (EOSV_BF16, EOSV_F32, EOSV_F32X3, MATCH_COSINE, MATCH_PROTONET, MAX_COLS, EosvDesc, check,
                    lib, ptr, stream_ptr)
 from .arch import SPECS
 
-_DTYPES = {"f32": EOSV_F32, "fp32": EOSV_F32, "float32": EOSV_F32, "bf16": EOSV_BF16, "bfloat16": EOSV_BF16}
+_DTYPES = {"f32": EOSV_F32, "fp32": EOSV_F32, "float32": EOSV_F32, "bf16": EOSV_BF16, "bfloat16": EOSV_BF16,
+           "f32x3": EOSV_F32X3}
 
 
 def _device(device) -> torch.device:

@@ -37,7 +37,11 @@ typedef enum {
 } eosv_status;
 
 typedef enum { EOSV_ARCH_R18 = 18, EOSV_ARCH_R50 = 50, EOSV_ARCH_R101 = 101 } eosv_arch;
-typedef enum { EOSV_F32 = 0, EOSV_BF16 = 1 } eosv_dtype;
+/* EOSV_F32X3: f32-accurate split-bf16 arithmetic.  Activations are stored as bf16 (hi, lo)
+ * pairs (hi = bf16(v), lo = bf16(v - hi): 16 significant bits), weights likewise, and every
+ * conv sums the three bf16 MFMA products hi.hi + lo.hi + hi.lo in f32 ("bf16x3"): ~2^-16
+ * relative per product, against 2^-8 for plain bf16.  The stem stays exact f32. */
+typedef enum { EOSV_F32 = 0, EOSV_BF16 = 1, EOSV_F32X3 = 2 } eosv_dtype;
 typedef enum { EOSV_MATCH_PROTONET = 0, EOSV_MATCH_COSINE = 1 } eosv_match_kind;
 
 typedef struct {
