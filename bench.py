@@ -161,6 +161,14 @@ def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches, chunks
     return (frames * per_frame + chunks * weights) / launches
 
 
+def print_layers(prof, tag):
+    ms, fl, nl = prof
+    for i in range(len(ms)):
+        if nl[i]:
+            print(f"[{tag}] layer {i:3d}: {ms[i] / nl[i]:8.3f} ms/launch  {fl[i] / ms[i] / 1e9:7.2f} TF/s",
+                  file=sys.stderr)
+
+
 def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
     ms, fl, nl = prof
     conv_ms, conv_fl = float(ms.sum()), float(fl.sum())
@@ -223,6 +231,8 @@ def main():
         el2, pred2, prof2, emb2 = run_timed(args, engine, arch_mod, synth, batches, dt2, local, dist)
         # clip embeddings of the last step vs the f32 primary: max over clips of
         # max|e - e_f32| / max|e_f32| (the north star's 1e-4 relative bound, tests/test_gpu_parity.py)
+        if args.layers and rank == 0:
+            print_layers(prof2, dt2)
         emb_rel = float((np.abs(emb2 - emb).max(1) / np.maximum(np.abs(emb).max(1), 1e-30)).max())
         preds2 = edist.gather_predictions(timed_idx, pred2.cpu().numpy(), len(plans))
         legs.append({"dtype": dt2, "value": round(clips / el2, 2), "unit": "clips/s",
@@ -265,10 +275,7 @@ def main():
         for i, leg in enumerate(legs):
             out["secondary" if i == 0 else "secondary_" + leg["dtype"]] = leg
         if args.layers:
-            for i in range(len(ms)):
-                if nl[i]:
-                    print(f"layer {i:3d}: {ms[i] / nl[i]:8.3f} ms/launch  {fl[i] / ms[i] / 1e9:7.2f} TF/s",
-                          file=sys.stderr)
+            print_layers(prof, args.dtype)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, [plans[e] for e in mine_idx[:50]], T)
         print(json.dumps(out), flush=True)

@@ -418,6 +418,9 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
   // K = 64 1x1 convs all measured slower than this choice
   const int v = bf16_variant();
+  // f32x3 (K tripled): 256x64 tiles for the Cout-64 stage-1 convs, +7 % over 128x64 (r01 A/B,
+  // tools/ab_x3.sh)
+  if (a.split && a.Cout <= 64 && v == 3) return launch_bf16<256, 64, 4, 1, false>(a, s);
   if (v == 8 && a.Cout == 128) return launch_bf16<256, 128, 4, 2, false, 3>(a, s);  // 144 KiB, 1 block/CU
   if (v == 9 && a.Cout == 128) return launch_bf16<128, 128, 2, 2, false, 3>(a, s);  // 96 KiB
   if ((v == 3 || v == 8 || v == 9) && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);

@@ -474,7 +474,7 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
     return !e || atoi(e) != 0;
   }();
   const bool sbf = stem_bf(h);  // EOSV_F32X3: exact-f32 stem with split output, bf16 blocks
-  const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W) : stem_pool_f32_ok(H, W));
+  const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W, direct) : stem_pool_f32_ok(H, W));
   if (x3(h) && !fused) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
   // the bf16 fused stem reads the f32 NCHW frames itself (no pack pass)
   const bool direct_bf = fused && sbf && direct;

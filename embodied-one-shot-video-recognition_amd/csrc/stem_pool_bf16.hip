@@ -68,6 +68,20 @@ __device__ __forceinline__ float row_shl(float v, int sh) {
                         : __builtin_amdgcn_update_dpp(0, iv, 0x102, 0xf, 0xf, false);
   return __int_as_float(r);
 }
+// value of the lane `sh` positions up within its 16-lane row; 0 past the row end (bound_ctrl),
+// so the compiler can fold it into the consuming v_max_f32 as a DPP source
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+// (lo, hi) -> one v_cvt_pk_bf16_f32 (round to nearest even)
+__device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
+  const bf16x2v p = __builtin_convertvector((f32x2v){lo, hi}, bf16x2v);
+  return __builtin_bit_cast(unsigned, p);
+}
+
+template <int SH>
+__device__ __forceinline__ float shl_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x100 + SH, 0xf, 0xf, true));
+}
 }  // namespace
 
 // x: padded bf16 RGB [N][H+6][Wp][3] (stem_row_pixels), w: [64][192] bf16, bias [64] f32,
@@ -308,11 +322,205 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-bool stem_pool_bf16_ok(int H, int W) {
+
+// Column-blocked DIRECT variant (the default for W % 4 == 0): a workgroup of CB_TILES = 4 waves
+// owns the pooled columns 28c .. 28c + 27 of one image (c = blockIdx.y), so two workgroups share
+// a CU (54 KiB LDS, 226 VGPRs = 2 waves per SIMD) and one's MFMAs run while the other converts
+// rows, pools, stores and waits at its barriers.  The full-width workgroup (8 waves, 1 per CU)
+// serialised those: r01 ablations (EOSV_STEM_ABL) put its DMA + pool + barrier skeleton alone
+// at 0.64 ms and its MFMAs alone at ~0.6 ms of 1.70 ms per 3200 frames.  No width limit: the
+// column blocks tile any W (ResNet-101 at 256 x 256 too).
+// Ring row of block c = padded-row bytes from 6 * pc0, pc0 = 28 * 4c - 2 (stem column 56c - 1
+// is its first: the left edge of pooled column 28c's window); a lane's k = its stem column
+// relative to that, + 1, so byte 12k of the row starts the lane's 7-pixel run, as before.
+constexpr int CB_TILES = 4;
+constexpr int CB_CH = (168 * CB_TILES + 72 + 15) / 16;  // 16-B chunks per ring copy (47)
+constexpr int CB_GP = 14 * CB_TILES + 5;               // column pairs per ring row (61)
+constexpr int CB_STG = 128;                             // f32 per staged plane row (32 lanes x 4)
+constexpr int CB_LDS = RING * 4 * CB_CH * 16;
+static_assert(12 * (CB_GP - 1) + 12 + 12 <= CB_CH * 16, "ring copy holds every pair at every shift");
+static_assert(2 * (CB_GP - 1) + 1 + 3 < CB_STG, "staged row covers every pair");
+static_assert(4 * CB_GP <= 64 * CB_TILES, "one conversion task per thread");
+
+__global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(const float* __restrict__ fx,
+                                                                        const u16* __restrict__ w,
+                                                                        const float* __restrict__ bias, u16* y,
+                                                                        int H, int W, int Hs, int Ws, int Hq, int Wq) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 12 * CB_STG * 4];
+  float* stg = (float*)(ring + CB_LDS);  // [row 4][plane 3][CB_STG]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: piece addressing on the SALU
+  const int r16 = lane & 15;
+  const int q = lane >> 4;
+  const int img = blockIdx.x;
+  const int t0 = blockIdx.y * CB_TILES;  // first 16-column MFMA tile of the block
+  const int pc0 = 28 * t0 - 2;           // padded column of ring pair 0
+  const int xs0 = 28 * t0 - 8;           // input column of staged element 0 (16-B aligned: W % 4 == 0)
+  const float* fimg = fx + (long long)img * 3 * H * W;
+
+  auto direct_load = [&](int prow, int g, float (&v)[6]) {
+    const int yy = prow - 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = pc0 + 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const float* src = fimg + (ok ? (long long)yy * W + xx : 0);  // always a valid address
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = src[(long long)c * H * W];
+        v[3 * h + c] = ok ? t : 0.f;
+      }
+    }
+  };
+  // 4 rows [r0, r0 + 4) x 3 planes -> staging: 12 pieces of 128 floats from column xs0, 3 per
+  // wave; 16-B pieces wholly outside the row read column 0 instead (never used: zero padding)
+  auto stage_f32 = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int p = wid + CB_TILES * i;
+      const int rr = p / 3, c = p - 3 * (p / 3);
+      const int yy = min(max(r0 + rr - 3, 0), H - 1);  // out-of-image rows: zeroed at conversion
+      const int xp = xs0 + 4 * lane;
+      const bool ok = xp >= 0 && xp + 4 <= W;
+      if (lane < CB_STG / 4)
+        dma16(fimg + ((long long)c * H + yy) * W + (ok ? xp : 0), stg + (rr * 3 + c) * CB_STG);
+    }
+  };
+  auto staged_load = [&](int prow, int rr, int g, float (&v)[6]) {
+    const int yy = prow - 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = pc0 + 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = stg[(rr * 3 + c) * CB_STG + 2 * g + h + 3];  // xx - xs0
+        v[3 * h + c] = ok ? t : 0.f;
+      }
+    }
+  };
+  auto direct_store = [&](int prow, int g, const float (&v)[6]) {
+    const unsigned d0 = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    const unsigned d1 = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    const unsigned d2 = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    unsigned char* slot = ring + (size_t)(((prow + 3) & (RING - 1)) * 4) * CB_CH * 16;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // copy m holds the row shifted by 4m bytes
+      unsigned* d = (unsigned*)(slot + (size_t)m * CB_CH * 16 + 12 * g + 4 * m);
+      d[0] = d0;
+      d[1] = d1;
+      d[2] = d2;
+    }
+  };
+
+  bf16x8 wf[4][6];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) wf[j][s] = *(const bf16x8*)(w + (j * 16 + r16) * KSTEM + 32 * s + 8 * q);
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(bias + j * 16 + 4 * q);
+
+  const int k = 14 * wid + r16;  // ring-relative stem column + 1
+  const int m = k & 3;
+  const int sx = 14 * (t0 + wid) - 1 + r16;
+  const float cmask = (sx >= 0 && sx < Ws) ? 0.f : -INFINITY;  // stem columns outside the map
+  const int xchunk = m * CB_CH + (12 * k + 4 * m) / 16;
+
+  auto stem_row = [&](int sy, f32x4 (&acc)[4]) {
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int g = 4 * s + q;
+      const int kh = min(g / 3, 6);  // kh 7: zero weights, any finite pixel
+      const int c = g - 3 * (g / 3);
+      const int slot = (2 * sy + kh + 3) & (RING - 1);
+      const bf16x8 xf = ((const bf16x8*)ring)[slot * 4 * CB_CH + xchunk + c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // s = 0 accumulates onto the BN shift (no per-step zeroing, no shift add)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xf, s ? acc[j] : bv[j], 0, 0, 0);
+    }
+  };
+
+  for (int t = tid; t < 13 * CB_GP; t += 64 * CB_TILES) {
+    float v[6];
+    direct_load(t / CB_GP, t % CB_GP, v);
+    direct_store(t / CB_GP, t % CB_GP, v);
+  }
+  __syncthreads();
+
+  const float NEG = -INFINITY;
+  f32x4 prev[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
+  u16* yimg = y + (long long)img * Hq * Wq * 64;
+  const int px = 7 * (t0 + wid) + (r16 >> 1);
+  const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
+  const bool dtask = tid < 4 * CB_GP;
+  const int drow = tid / CB_GP, dg = tid - (tid / CB_GP) * CB_GP;
+#pragma unroll 2  // prev alternates registers instead of 16 copies per step
+  for (int py = 0; py < Hq; ++py) {
+    if (py + 1 < Hq) stage_f32(4 * py + 9);
+    f32x4 a1[4], a2[4];
+    stem_row(2 * py, a1);
+    stem_row(2 * py + 1, a2);
+    // Pool on the accumulators, which start from the BN shift (max commutes with ReLU and the bf16
+    // rounding, both monotone).  VALU-lean: the SIMD's vector issue, not the MFMA pipe, bounded
+    // this loop (r01: ~290 VALU per wave-step against 48 MFMAs): Hs is even (launcher), so no stem
+    // row is past the map; the column mask is one add of 0 / -inf after the row max; the column
+    // max takes its neighbours by DPP (bound_ctrl: lanes past the 16-lane row read 0, they are
+    // not writers); the file is built with -fno-honor-nans (no canonicalising max per DPP value).
+    unsigned pk4[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int e2 = 0; e2 < 2; ++e2) {
+        float o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * e2 + h;
+          const float v = fmaxf(fmaxf(prev[j][e], a1[j][e]), a2[j][e]) + cmask;  // row max
+          prev[j][e] = a2[j][e];
+          const float c = fmaxf(fmaxf(v, shl_dpp<1>(v)), shl_dpp<2>(v));
+          o[h] = fmaxf(c, 0.f);  // the shift is in the accumulators
+        }
+        pk4[j][e2] = pack_bf2(o[0], o[1]);
+      }
+    }
+    if (py + 1 < Hq) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (dtask) {
+        float dv[6];
+        staged_load(4 * py + 9 + drow, drow, dg, dv);
+        direct_store(4 * py + 9 + drow, dg, dv);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (writer)
+        *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk4[j][0], pk4[j][1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+static bool stem_cb() {
+  static const bool v = [] {
+    const char* e = getenv("EOSV_STEM_CB");  // 0 = full-width workgroups (A/B switch)
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// direct: the caller passes the f32 NCHW frames (no pack)
+bool stem_pool_bf16_ok(int H, int W, bool direct) {
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Wq = (Ws + 2 - 3) / 2 + 1;
-  (void)Hs;
-  return H >= 8 && W >= 8 && (Wq + 6) / 7 <= MAX_TILES;
+  if (H < 8 || W < 8) return false;
+  return (direct && stem_cb() && W % 4 == 0 && Hs % 2 == 0) || (Wq + 6) / 7 <= MAX_TILES;
 }
 
 // pack: padded bf16 RGB rows (pack_rgb_pad), or nullptr with `frames` = the f32 NCHW input
@@ -321,6 +529,14 @@ int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, 
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int ntiles = (Wq + 6) / 7;
+  if (frames && stem_cb() && W % 4 == 0 && Hs % 2 == 0) {
+    if (B <= 0) return EOSV_OK;
+    const int ncb = (ntiles + CB_TILES - 1) / CB_TILES;
+    hipLaunchKernelGGL(stem_pool_bf16_cb_kernel, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w, bias,
+                       (u16*)y, H, W, Hs, Ws, Hq, Wq);
+    EOSV_LAUNCH_CHECK();
+    return EOSV_OK;
+  }
   if (ntiles > MAX_TILES || B <= 0) return B <= 0 ? EOSV_OK : (set_error("stem_pool: too wide"), EOSV_ERR_UNSUPPORTED);
   const int Wp = stem_row_pixels(W, 3);
   if (frames) {

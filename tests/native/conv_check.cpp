@@ -316,6 +316,11 @@ int main() {
   fails += check_stem_pool(2, 224, 224, true);
   fails += check_stem_pool(3, 100, 86, true);
   fails += check_stem_pool(2, 64, 48, true);
+  // column-blocked direct kernel (W % 4 == 0): ResNet-101's 256 x 256 (3 column blocks, the last
+  // half idle), a ragged last block, a single partial block
+  if (stem_pool_bf16_ok(256, 256, true)) fails += check_stem_pool(2, 256, 256, true);  // (EOSV_STEM_CB=0: unfused)
+  fails += check_stem_pool(3, 100, 88, true);
+  fails += check_stem_pool(2, 60, 36, true);
   fails += check_stem_pool_f32(2, 224, 224);
   fails += check_stem_pool_f32(3, 100, 86);
   fails += check_stem_pool_f32(2, 64, 48);
