@@ -45,6 +45,8 @@ struct ConvArgs {
   const void* zero;   // >= 64 zeroed bytes (DMA target for out-of-bounds taps)
   int abl;            // ablation bits for profiling builds (0 = normal)
   int xcd;            // 1: XCD-aware block order (each XCD walks a contiguous range of tiles)
+  int p8pipe;         // conv_bf16_p8: 1 counted-vmcnt half-tile pipeline, 0 former vmcnt(0) per K-tile
+  int p8prio;         // conv_bf16_p8: 1 s_setprio(1) around the MFMA segments
   int kcm;            // bf16 only: K ordered (cin/64, kh, kw, cin%64) instead of (kh, kw, cin)
   // fused 1x1 downsample (ResNet block shortcut): K columns [K1, K) read x2 at output pixel
   // (oh, ow) -> x2 pixel (oh * stride2, ow * stride2), channel k - K1; nullptr = none
@@ -73,6 +75,9 @@ int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 bool stem_pool_bf16_ok(int H, int W, bool direct);  // stem_pool_bf16.hip: fused stem conv + ReLU + maxpool
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                           hipStream_t s, const float* frames = nullptr);
+bool stem_pool_x3_ok(int H, int W);  // stem_pool_bf16.hip: EOSV_F32X3 split-bf16 fused stem
+int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w, const float* bias, void* y,
+                        hipStream_t s);
 bool stem_pool_f32_ok(int H, int W);  // stem_pool_f32.hip: the same for f32
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                          hipStream_t s, bool split = false);  // split: y in the EOSV_F32X3 (hi, lo, hi) layout

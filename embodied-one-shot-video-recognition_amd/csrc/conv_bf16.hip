@@ -52,6 +52,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int M = a.N * HoWo;
   const int nN = (a.Cout + BN - 1) / BN;
   const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
+  if (a.abl & 512) return;  // profiling-only: dispatch cost alone
   const int mt = bt / nN;
   const int nt = bt - mt * nN;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int r = lane & (MF - 1);
   const int q = lane / MF;
   const int sw = (r >> 1) & 7;  // tile bases are multiples of 16 rows: the swizzle depends on r only
-  const int nk = a.K / BK;
+  const int nk = (a.abl & 1024) ? 0 : a.K / BK;  // 1024 (profiling-only): no K-loop
   // NS-deep ring: NS-1 stages in flight; with NS = 3 the wait before each barrier is a
   // counted vmcnt (the newest stage stays in flight across it) and barriers are raw
   // s_barrier (__syncthreads would drain it with vmcnt(0))
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
     // a.abl (profiling-only ablations, results wrong when set): 1 no main-loop loads,
-    // 4 no A loads, 8 no B loads, 2 no output stores
+    // 4 no A loads, 8 no B loads, 2 no output stores, 16 no ds_reads, 32 no MFMAs, 64 no epilogue
     if (issue && !(a.abl & 1)) stage((kt + NS - 1) * BK, wslot, a.abl);
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
@@ -194,10 +195,21 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     for (int s = 0; s < BK / KS; ++s) {
       const int pch = ((s * (KS / 8) + q) ^ sw) * 8;
       bf16x8 af[TM], bf[TN];
+      if (a.abl & 16) {  // profiling-only: no ds_reads (operands stay whatever the registers hold)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(As + (wm * (BM / WM) + i * MF + r) * BK + pch);
+        for (int i = 0; i < TM; ++i) af[i] = bf16x8{};
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * MF + r) * BK + pch);
+        for (int j = 0; j < TN; ++j) bf[j] = bf16x8{};
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(As + (wm * (BM / WM) + i * MF + r) * BK + pch);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * MF + r) * BK + pch);
+      }
+      if (a.abl & 32) {  // profiling-only: no MFMAs
+        asm volatile("" ::"v"(af[0]), "v"(bf[0]));
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -218,6 +230,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     wslot = wslot + 1 == NS ? 0 : wslot + 1;
   }
 
+  if (a.abl & 64) {  // profiling-only: no epilogue
+    asm volatile("" ::"v"(acc[0][0][0]));
+    return;
+  }
   u16* __restrict__ y = (u16*)a.y;
   const u16* __restrict__ res = (const u16*)a.res;
   // Epilogue staged through LDS (the ring is free now): pass i moves the i-th 32-row

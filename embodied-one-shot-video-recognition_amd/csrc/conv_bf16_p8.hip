@@ -14,11 +14,17 @@
 //     reuse the registers already loaded: 12, 4, 8, 4 ds_read_b128 per phase.
 //   * waves 4-7 (the SIMD partners of waves 0-3) run one barrier behind, so on every SIMD one
 //     wave is in its MFMA segment while its partner reads LDS and issues DMA.
-//   * 2 LDS buffers; K-tile t+1's DMA is issued in phases 0 (A) and 1 (B) of K-tile t and
-//     retired by a vmcnt(0) in the LOAD segment of phase 3, two phases later.  WAR: a buffer is
-//     re-staged only after every wave passed the barrier that ends its last LOAD segment on it
-//     (each LOAD segment ends with lgkmcnt(0)); RAW: the vmcnt(0) sits before a barrier that
-//     every reader of the buffer passes before its first ds_read of it.
+//   * 2 LDS buffers, each K-tile staged as 4 half-tiles: A-top (the A0-3 rows of every wave
+//     row), B-left (B0-1), B-right (B2-3), A-bottom (A4-7); every wave issues the same number of
+//     DMA pieces of each.  K-tile t+1's half-tiles go out one per phase of K-tile t, in the order
+//     its phases consume them, and each is retired by a COUNTED vmcnt one phase before its first
+//     reader (3 half-tiles stay in flight across the barriers, cdna_hip_programming.md T3+T4):
+//     a half-tile gets ~4 phases of MFMA time to land instead of ~2.5 with the former
+//     "all of t+1 in phases 0-1, vmcnt(0) in phase 3" (EOSV_P8_PIPE=0 keeps that for A/B).
+//     WAR: a region of buffer (t+1)&1 is re-staged 3+ barriers after its last LOAD segment in
+//     K-tile t-1 (waves 4-7 trail by one); RAW: each wait sits before a barrier that every
+//     reader passes before its first ds_read of the region.
+//   * s_setprio(1) around each MFMA segment (T5; EOSV_P8_PRIO=0 drops it).
 // Epilogue as conv_bf16.hip: bias (+ residual) (+ ReLU) through an LDS-staged f32 tile so that
 // residual loads and output stores are 16 B per lane.
 #include <hip/hip_bf16.h>
@@ -83,9 +89,15 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
     xr2 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const u16*)a.x2 + (long long)img0 * a.H2 * a.W2 * a.Cin2), (short)0,
         (int)((long long)(img1 - img0 + 1) * a.H2 * a.W2 * a.Cin2 * 2), 0x00020000);
+  // A piece j: half h = j / (AI/2) (0: rows 0-63 of each 128-row wave strip = A0-3, 1: rows
+  // 64-127 = A4-7), 8 consecutive rows of that half; arow0[j] = the piece's first LDS row
+  int arow0[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
-    const int row = wid * (BM / NW) + 8 * j + lr;
+    const int h = j / (AI / 2), jj = j % (AI / 2);
+    const int idx0 = wid * (BM / 2 / NW) + 8 * jj;  // in the half's row list (64 per strip)
+    arow0[j] = (idx0 / 64) * 128 + h * 64 + idx0 % 64;
+    const int row = arow0[j] + lr;
     const int lc = pc ^ ((row >> 1) & 7);
     const int m = m0 + row;
     amask[j] = 0;
@@ -105,10 +117,15 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
           if ((unsigned)(ih + kh) < (unsigned)a.H && (unsigned)(iw + kw) < (unsigned)a.W) amask[j] |= 1u << (kh * a.KW + kw);
     }
   }
+  // B piece j: half h = j / (BI/2) (0: cols 0-31 of each 64-col wave strip = B0-1, 1: 32-63 = B2-3)
   const u16* brow[BI];
+  int brow0[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
-    const int row = wid * (BN / NW) + 8 * j + lr;
+    const int h = j / (BI / 2), jj = j % (BI / 2);
+    const int idx0 = wid * (BN / 2 / NW) + 8 * jj;  // in the half's row list (32 per strip)
+    brow0[j] = (idx0 / 32) * 64 + h * 32 + idx0 % 32;
+    const int row = brow0[j] + lr;
     const int lc = pc ^ ((row >> 1) & 7);
     const int n = n0 + row;
     brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 8 : nullptr;
@@ -146,30 +163,31 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
       }
     }
   };
-  auto stage_a = [&](u16* As) {
+  // stage half h of A (B) of the K-tile the walk state points at into As (Bs)
+  auto stage_a = [&](u16* As, int h) {
     if (DS && kk >= a.K1) {
       const int d = (kk - a.K1) * 2;
 #pragma unroll
-      for (int j = 0; j < (DS ? AI : 1); ++j) {
-        const int voff = aoffs2[j] >= 0 ? aoffs2[j] + d : (int)0x80000000;
-        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+      for (int j = h * (AI / 2); j < (h + 1) * (AI / 2); ++j) {
+        const int voff = aoffs2[DS ? j : 0] >= 0 ? aoffs2[DS ? j : 0] + d : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, (__attribute__((address_space(3))) void*)(As + arow0[j] * BK), 16,
+                                                 voff, 0, 0, 0);
       }
       return;
     }
 #pragma unroll
-    for (int j = 0; j < AI; ++j) {
+    for (int j = h * (AI / 2); j < (h + 1) * (AI / 2); ++j) {
       const int voff = ((amask[j] >> tap) & 1) ? aoffs[j] + toff : (int)0x80000000;
-      u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + arow0[j] * BK), 16, voff,
+                                               0, 0, 0);
     }
   };
-  auto stage_b = [&](int k0, u16* Bs) {
+  auto stage_b = [&](int k0, u16* Bs, int h) {
 #pragma unroll
-    for (int j = 0; j < BI; ++j) {
+    for (int j = h * (BI / 2); j < (h + 1) * (BI / 2); ++j) {
       const u16* src = brow[j] ? brow[j] + k0 : zero;
-      u16* dst = Bs + (wid * (BN / NW) + 8 * j) * BK;
-      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(Bs + brow0[j] * BK), 16,
+                                       0, 0);
     }
   };
 
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
   const int boff = BM * BK + (wn * 64 + r) * BK;
   bf16x8 af[4][2] = {}, bfr[2][2] = {};
   // a.abl (profiling-only ablations, results wrong when set): 1 no main-loop DMA,
-  // 16 no main-loop ds_reads, 32 no MFMAs
+  // 16 no main-loop ds_reads, 32 no MFMAs, 256 no epilogue
   auto read_a = [&](const u16* S, int i0) {
     if (a.abl & 16) return;
 #pragma unroll
@@ -222,58 +240,120 @@ __global__ __launch_bounds__(512) void conv_bf16_p8_kernel(ConvArgs a) {
   // end of a LOAD segment: own LDS reads retired (WAR safety for the next re-stage), then
   // the barrier that opens the MFMA segment; the MFMA segment ends with another barrier
   const bool nobar = a.abl & 128;
+  const bool prio = a.p8prio;
 #define P8_LOAD_END()                                   \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
   if (!nobar) __builtin_amdgcn_s_barrier();             \
-  __builtin_amdgcn_sched_barrier(0)
-#define P8_MFMA_END()              \
-  __builtin_amdgcn_sched_barrier(0); \
+  __builtin_amdgcn_sched_barrier(0);                    \
+  if (prio) __builtin_amdgcn_s_setprio(1)
+#define P8_MFMA_END()                       \
+  __builtin_amdgcn_sched_barrier(0);        \
+  if (prio) __builtin_amdgcn_s_setprio(0);  \
   if (!nobar) __builtin_amdgcn_s_barrier(); \
   __builtin_amdgcn_sched_barrier(0)
+#define P8_VMCNT(N) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory")
+  constexpr int HA = AI / 2, HB = BI / 2;  // DMA instructions per half-tile per wave
 
   const int nk = a.K / BK;
-  stage_a(smem);
-  stage_b(0, smem + BM * BK);
+  stage_a(smem, 0);
+  stage_a(smem, 1);
+  stage_b(0, smem + BM * BK, 0);
+  stage_b(0, smem + BM * BK, 1);
   advance();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (half) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
   __builtin_amdgcn_sched_barrier(0);
-  for (int t = 0; t < nk; ++t) {
-    const u16* S = smem + (t & 1) * STAGE;
-    u16* Nx = smem + ((t & 1) ^ 1) * STAGE;
-    const bool more = t + 1 < nk && !(a.abl & 1);
-    // phase 0: A0-3, B0-1
-    read_a(S, 0);
-    read_b(S, 0);
-    if (more && !(a.abl & 512)) stage_a(Nx);
-    advance();
-    P8_LOAD_END();
-    mfma(0, 0);
-    P8_MFMA_END();
-    // phase 1: B2-3
-    read_b(S, 2);
-    if (more && !(a.abl & 1024)) stage_b((t + 1) * BK, Nx + BM * BK);
-    P8_LOAD_END();
-    mfma(0, 2);
-    P8_MFMA_END();
-    // phase 2: A4-7
-    read_a(S, 4);
-    P8_LOAD_END();
-    mfma(4, 2);
-    P8_MFMA_END();
-    // phase 3: B0-1; retire K-tile t+1's DMA before the barrier its readers pass first
-    read_b(S, 0);
-    if (more && !(a.abl & 64)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    P8_LOAD_END();
-    mfma(4, 0);
-    P8_MFMA_END();
+  if (a.p8pipe) {
+    for (int t = 0; t < nk; ++t) {
+      const u16* S = smem + (t & 1) * STAGE;
+      u16* Nx = smem + ((t & 1) ^ 1) * STAGE;
+      const bool more = t + 1 < nk && !(a.abl & 1);
+      // phase 0: A0-3, B0-1; issue A-top(t+1); retire B-right(t) (younger: A-bottom(t), A-top(t+1))
+      read_a(S, 0);
+      read_b(S, 0);
+      if (more) {
+        stage_a(Nx, 0);
+        P8_VMCNT(2 * HA);
+      } else {
+        P8_VMCNT(HA);
+      }
+      P8_LOAD_END();
+      mfma(0, 0);
+      P8_MFMA_END();
+      // phase 1: B2-3; issue B-left(t+1); retire A-bottom(t) (younger: A-top(t+1), B-left(t+1))
+      read_b(S, 2);
+      if (more) {
+        stage_b((t + 1) * BK, Nx + BM * BK, 0);
+        P8_VMCNT(HA + HB);
+      } else {
+        P8_VMCNT(0);
+      }
+      P8_LOAD_END();
+      mfma(0, 2);
+      P8_MFMA_END();
+      // phase 2: A4-7; issue B-right(t+1)
+      read_a(S, 4);
+      if (more) stage_b((t + 1) * BK, Nx + BM * BK, 1);
+      P8_LOAD_END();
+      mfma(4, 2);
+      P8_MFMA_END();
+      // phase 3: B0-1; issue A-bottom(t+1); retire A-top(t+1), B-left(t+1) (younger: B-right(t+1),
+      // A-bottom(t+1)) before the barrier that K-tile t+1's phase-0 readers pass
+      read_b(S, 0);
+      if (more) {
+        stage_a(Nx, 1);
+        P8_VMCNT(HB + HA);
+      }
+      advance();
+      P8_LOAD_END();
+      mfma(4, 0);
+      P8_MFMA_END();
+    }
+  } else {
+    for (int t = 0; t < nk; ++t) {
+      const u16* S = smem + (t & 1) * STAGE;
+      u16* Nx = smem + ((t & 1) ^ 1) * STAGE;
+      const bool more = t + 1 < nk && !(a.abl & 1);
+      read_a(S, 0);
+      read_b(S, 0);
+      if (more && !(a.abl & 512)) {
+        stage_a(Nx, 0);
+        stage_a(Nx, 1);
+      }
+      advance();
+      P8_LOAD_END();
+      mfma(0, 0);
+      P8_MFMA_END();
+      read_b(S, 2);
+      if (more && !(a.abl & 1024)) {
+        stage_b((t + 1) * BK, Nx + BM * BK, 0);
+        stage_b((t + 1) * BK, Nx + BM * BK, 1);
+      }
+      P8_LOAD_END();
+      mfma(0, 2);
+      P8_MFMA_END();
+      read_a(S, 4);
+      P8_LOAD_END();
+      mfma(4, 2);
+      P8_MFMA_END();
+      read_b(S, 0);
+      if (more && !(a.abl & 64)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      P8_LOAD_END();
+      mfma(4, 0);
+      P8_MFMA_END();
+    }
   }
   if (!half) __builtin_amdgcn_s_barrier();  // re-align the halves
 #undef P8_LOAD_END
 #undef P8_MFMA_END
+#undef P8_VMCNT
   __syncthreads();
 
+  if (a.abl & 256) {  // profiling-only: no epilogue
+    asm volatile("" ::"v"(acc[0][0][0]));
+    return;
+  }
   u16* __restrict__ y = (u16*)a.y;
   const u16* __restrict__ res = (const u16*)a.res;
   // Epilogue staged through LDS (the buffers are free now): pass i moves the i-th 32-row
@@ -396,7 +476,16 @@ bool conv_bf16_p8_ok(const ConvArgs& a) {
 bool conv_bf16_p8_default(const ConvArgs& a) { return a.Cout == 128 && a.stride == 1 && a.K >= 576; }
 // (with a fused downsample, a.K includes its Cin2 columns; the shape test above is unchanged)
 
-int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s) {
+static int p8_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+int launch_conv_bf16_p8(const ConvArgs& a0, hipStream_t s) {
+  static const int pipe = p8_env("EOSV_P8_PIPE", 1), prio = p8_env("EOSV_P8_PRIO", 1);  // A/B switches
+  ConvArgs a = a0;
+  a.p8pipe = pipe;
+  a.p8prio = prio;
   if (!conv_bf16_p8_ok(a)) return set_error("conv_bf16_p8: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const int BM = a.Cout == 128 ? 512 : 256;

@@ -46,6 +46,7 @@ struct eosv_handle {
   int D = 0;
   int hs = 0, ws = 0, hp = 0, wp = 0;  // stem / maxpool output sizes
   eosv::Conv stem, fc;
+  eosv::Conv stem_x3;  // EOSV_F32X3 split-bf16 stem: w = [hi | lo] [64][192] bf16 (stem_pool_bf16.hip)
   std::vector<eosv::Block> blocks;
   bool loaded = false;
   size_t act_elems = 0;  // per-frame max activation elements
@@ -473,13 +474,19 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
     const char* e = getenv("EOSV_STEM_DIRECT");  // 0 = pack kernel + LDS-DMA rows (A/B switch)
     return !e || atoi(e) != 0;
   }();
-  const bool sbf = stem_bf(h);  // EOSV_F32X3: exact-f32 stem with split output, bf16 blocks
+  static const bool x3_split_stem = [] {
+    const char* e = getenv("EOSV_X3_STEM");  // 0 = exact-f32 MFMA stem for EOSV_F32X3 (A/B switch)
+    return !e || atoi(e) != 0;
+  }();
+  const bool sbf = stem_bf(h);  // EOSV_F32X3: split-bf16 (or exact-f32) stem with split output, bf16 blocks
+  // EOSV_F32X3: the split-bf16 fused stem reads the f32 frames directly
+  const bool x3stem = x3(h) && direct && x3_split_stem && h->stem_x3.w && stem_pool_x3_ok(H, W);
   const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W, direct) : stem_pool_f32_ok(H, W));
-  if (x3(h) && !fused) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
+  if (x3(h) && !fused && !x3stem) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
   // the bf16 fused stem reads the f32 NCHW frames itself (no pack pass)
   const bool direct_bf = fused && sbf && direct;
-  if (!direct_bf && (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s))) return rc;
-  if (fused) {
+  if (!direct_bf && !x3stem && (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s))) return rc;
+  if (fused || x3stem) {
     // fused stem conv + ReLU + maxpool (profiled as the stem layer)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) {
@@ -488,9 +495,10 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
       if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
       EOSV_HIP_CHECK(hipEventRecord(e0, s));
     }
-    if ((rc = sbf ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
-                                          direct_bf ? frames : nullptr)
-                  : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s, x3(h))))
+    if ((rc = x3stem ? launch_stem_pool_x3(frames, B, H, W, h->stem_x3.w, h->stem_x3.b, bufs[1], s)
+              : sbf  ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
+                                             direct_bf ? frames : nullptr)
+                     : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s, x3(h))))
       return rc;
     if (h->prof) {
       EOSV_HIP_CHECK(hipEventRecord(e1, s));
@@ -598,6 +606,23 @@ int eosv_load_weights(eosv_handle* h, const char* const* names, const void* cons
   int rc;
   h->loaded = false;
   if ((rc = upload_conv(h, h->stem, t, stem_bf(h), true))) return rc;
+  if (sp) {  // split-bf16 stem weights: the bf16 stem layout (K 192), as hi and lo = bf16(w - hi)
+    Conv c = h->stem;
+    c.K = 192;
+    std::vector<float> wf, beta;
+    if (!fold_conv(c, t, true, true, wf, beta)) return EOSV_ERR_ARG;
+    std::vector<unsigned short> wb(2 * wf.size());
+    for (size_t i = 0; i < wf.size(); ++i) {
+      const float hi = bf_round_host(wf[i]);
+      wb[i] = f2bf_host(hi);
+      wb[wf.size() + i] = f2bf_host(wf[i] - hi);
+    }
+    if ((rc = dmalloc(h, &c.w, wb.size() * 2))) return rc;
+    EOSV_HIP_CHECK(hipMemcpy(c.w, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+    if ((rc = dmalloc(h, (void**)&c.b, (size_t)c.cout * 4))) return rc;
+    EOSV_HIP_CHECK(hipMemcpy(c.b, beta.data(), (size_t)c.cout * 4, hipMemcpyHostToDevice));
+    h->stem_x3 = c;
+  }
   for (Block& b : h->blocks) {
     if ((rc = upload_conv(h, b.c1, t, bf, true, nullptr, sp))) return rc;
     Conv* fds = b.fuse_ds ? &b.ds : nullptr;

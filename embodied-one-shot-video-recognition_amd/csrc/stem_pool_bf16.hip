@@ -459,7 +459,6 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
   const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
   const bool dtask = tid < 4 * CB_GP;
   const int drow = tid / CB_GP, dg = tid - (tid / CB_GP) * CB_GP;
-#pragma unroll 2  // prev alternates registers instead of 16 copies per step
   for (int py = 0; py < Hq; ++py) {
     if (py + 1 < Hq) stage_f32(4 * py + 9);
     f32x4 a1[4], a2[4];
@@ -505,6 +504,238 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
+// EOSV_F32X3 stem (column-blocked, DIRECT frames): the same fused stem conv + ReLU + maxpool in
+// split-bf16 arithmetic.  Frames are split as x = x_hi + x_lo and the folded weights as
+// w = w_hi + w_lo (each part bf16, round to nearest), and every MFMA k-slice accumulates
+// w_hi.x_hi + w_hi.x_lo + w_lo.x_hi in f32 (the x_lo.w_lo term, ~2^-16 relative, is dropped, as
+// in the split convs; tests/test_gpu_parity.py bounds the features at 1e-4 of the f32 oracle).
+// Replaces the exact-f32 MFMA stem (v_mfma_f32_16x16x4_f32: 16x fewer FLOP/clk than bf16).
+// Output: pooled map in the split layout [pixel][hi 64 | lo 64 | hi 64].
+// LDS (56 KiB -> 2 workgroups per CU): w_lo [64][192] (16-B chunk c of row r at
+// (c & ~7) | ((c ^ (r >> 1)) & 7): conflict-free A-fragment reads); x_hi and x_lo rings, ONE copy
+// each (16 rows x 736 B), read as 4 dwords per B fragment (4-B aligned sources: no shifted
+// copies); the f32 staging of the DIRECT kernel.  w_hi stays in registers.
+constexpr int X3_ROWB = 736;  // bytes per ring row: 12 * CB_GP = 732, rounded up to 16
+static_assert(12 * CB_GP <= X3_ROWB, "x3 ring row");
+constexpr int X3_RING = RING * X3_ROWB;                 // bytes per ring (hi or lo)
+constexpr int X3_WLO = 64 * KSTEM * 2;                  // bytes of w_lo
+
+__global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_x3_cb_kernel(const float* __restrict__ fx,
+                                                                          const u16* __restrict__ w,
+                                                                          const float* __restrict__ bias, u16* y,
+                                                                          int H, int W, int Hs, int Ws, int Hq, int Wq) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[X3_WLO + 2 * X3_RING + 12 * CB_STG * 4];
+  u16* wlo_s = (u16*)lds;
+  unsigned char* rh = lds + X3_WLO;           // x_hi ring
+  unsigned char* rl = rh + X3_RING;           // x_lo ring
+  float* stg = (float*)(rl + X3_RING);        // [row 4][plane 3][CB_STG]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15;
+  const int q = lane >> 4;
+  const int img = blockIdx.x;
+  const int t0 = blockIdx.y * CB_TILES;
+  const int pc0 = 28 * t0 - 2;
+  const int xs0 = 28 * t0 - 8;
+  const float* fimg = fx + (long long)img * 3 * H * W;
+
+  // w_lo -> LDS (swizzled 16-B chunks), w_hi -> registers
+  for (int i = tid; i < 64 * (KSTEM / 8); i += 64 * CB_TILES) {
+    const int r = i / (KSTEM / 8), c = i - r * (KSTEM / 8);
+    const int cs = (c & ~7) | ((c ^ (r >> 1)) & 7);
+    *(uint4*)(wlo_s + r * KSTEM + cs * 8) = *(const uint4*)(w + 64 * KSTEM + r * KSTEM + c * 8);
+  }
+  bf16x8 wf[4][6];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) wf[j][s] = *(const bf16x8*)(w + (j * 16 + r16) * KSTEM + 32 * s + 8 * q);
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(bias + j * 16 + 4 * q);
+
+  auto direct_load = [&](int prow, int g, float (&v)[6]) {
+    const int yy = prow - 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = pc0 + 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const float* src = fimg + (ok ? (long long)yy * W + xx : 0);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = src[(long long)c * H * W];
+        v[3 * h + c] = ok ? t : 0.f;
+      }
+    }
+  };
+  auto stage_f32 = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int p = wid + CB_TILES * i;
+      const int rr = p / 3, c = p - 3 * (p / 3);
+      const int yy = min(max(r0 + rr - 3, 0), H - 1);
+      const int xp = xs0 + 4 * lane;
+      const bool ok = xp >= 0 && xp + 4 <= W;
+      if (lane < CB_STG / 4)
+        dma16(fimg + ((long long)c * H + yy) * W + (ok ? xp : 0), stg + (rr * 3 + c) * CB_STG);
+    }
+  };
+  auto staged_load = [&](int prow, int rr, int g, float (&v)[6]) {
+    const int yy = prow - 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = pc0 + 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = stg[(rr * 3 + c) * CB_STG + 2 * g + h + 3];
+        v[3 * h + c] = ok ? t : 0.f;
+      }
+    }
+  };
+  // pair g of padded row prow -> 12 B of the hi ring row and 12 B of the lo ring row
+  auto direct_store = [&](int prow, int g, const float (&v)[6]) {
+    unsigned hi[3], lo[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const unsigned ph = pack_bf2(v[2 * i], v[2 * i + 1]);
+      hi[i] = ph;
+      lo[i] = pack_bf2(v[2 * i] - __uint_as_float(ph << 16), v[2 * i + 1] - __uint_as_float(ph & 0xffff0000u));
+    }
+    const int off = ((prow + 3) & (RING - 1)) * X3_ROWB + 12 * g;
+    unsigned* dh = (unsigned*)(rh + off);
+    unsigned* dl = (unsigned*)(rl + off);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      dh[i] = hi[i];
+      dl[i] = lo[i];
+    }
+  };
+
+  const int k = 14 * wid + r16;  // ring-relative stem column + 1
+  const int sx = 14 * (t0 + wid) - 1 + r16;
+  const float cmask = (sx >= 0 && sx < Ws) ? 0.f : -INFINITY;
+  // per k-slice s: this lane's B-fragment byte offset in a ring row, and its w_lo A-fragment chunk
+  int xoff[6], khs[6];
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int g = 4 * s + q;
+    khs[s] = min(g / 3, 6);  // kh 7: zero weights, any finite pixel
+    xoff[s] = 12 * k + 16 * (g - 3 * (g / 3));
+  }
+  auto ldx = [&](const unsigned char* ring, int row, int s) {
+    const unsigned* p = (const unsigned*)(ring + ((row + khs[s] + 3) & (RING - 1)) * X3_ROWB + xoff[s]);
+    unsigned v[4] = {p[0], p[1], p[2], p[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto stem_rows = [&](int sy0, f32x4 (&a1)[4], f32x4 (&a2)[4]) {
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      bf16x8 wl[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = j * 16 + r16, c = 4 * s + q;
+        wl[j] = *(const bf16x8*)(wlo_s + r * KSTEM + ((c & ~7) | ((c ^ (r >> 1)) & 7)) * 8);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        f32x4(&acc)[4] = rr ? a2 : a1;
+        const int row = 2 * (sy0 + rr);
+        const bf16x8 xh = ldx(rh, row, s), xl = ldx(rl, row, s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xh, s ? acc[j] : bv[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[j], xh, acc[j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  for (int t = tid; t < 13 * CB_GP; t += 64 * CB_TILES) {
+    float v[6];
+    direct_load(t / CB_GP, t % CB_GP, v);
+    direct_store(t / CB_GP, t % CB_GP, v);
+  }
+  __syncthreads();
+
+  const float NEG = -INFINITY;
+  f32x4 prev[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
+  u16* yimg = y + (long long)img * Hq * Wq * 192;
+  const int px = 7 * (t0 + wid) + (r16 >> 1);
+  const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
+  const bool dtask = tid < 4 * CB_GP;
+  const int drow = tid / CB_GP, dg = tid - (tid / CB_GP) * CB_GP;
+  for (int py = 0; py < Hq; ++py) {
+    if (py + 1 < Hq) stage_f32(4 * py + 9);
+    f32x4 a1[4], a2[4];
+    stem_rows(2 * py, a1, a2);
+    // pool as stem_pool_bf16_cb_kernel (Hs even: no stem row past the map), then split the
+    // pooled f32 value into hi + lo
+    uint2 ph[4], pl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = fmaxf(fmaxf(prev[j][e], a1[j][e]), a2[j][e]) + cmask;
+        prev[j][e] = a2[j][e];
+        const float c = fmaxf(fmaxf(v, shl_dpp<1>(v)), shl_dpp<2>(v));
+        o[e] = fmaxf(c, 0.f);
+      }
+      const unsigned h0 = pack_bf2(o[0], o[1]), h1 = pack_bf2(o[2], o[3]);
+      ph[j] = make_uint2(h0, h1);
+      pl[j] = make_uint2(pack_bf2(o[0] - __uint_as_float(h0 << 16), o[1] - __uint_as_float(h0 & 0xffff0000u)),
+                         pack_bf2(o[2] - __uint_as_float(h1 << 16), o[3] - __uint_as_float(h1 & 0xffff0000u)));
+    }
+    if (py + 1 < Hq) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (dtask) {
+        float dv[6];
+        staged_load(4 * py + 9 + drow, drow, dg, dv);
+        direct_store(4 * py + 9 + drow, dg, dv);
+      }
+    }
+    if (writer) {
+      u16* o = yimg + ((long long)py * Wq + px) * 192 + 4 * q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        *(uint2*)(o + j * 16) = ph[j];
+        *(uint2*)(o + 64 + j * 16) = pl[j];
+        *(uint2*)(o + 128 + j * 16) = ph[j];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool stem_pool_x3_ok(int H, int W) {
+  const int Hs = (H + 6 - 7) / 2 + 1;
+  return H >= 8 && W >= 8 && W % 4 == 0 && Hs % 2 == 0;
+}
+
+// w: [hi 64 x 192 | lo 64 x 192] bf16 (stem K layout [kh 8][24]), bias f32 [64], frames f32 NCHW,
+// y: split layout [N][Hq][Wq][192]
+int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w, const float* bias, void* y,
+                        hipStream_t s) {
+  if (!stem_pool_x3_ok(H, W)) return set_error("stem_pool_x3: unsupported frame shape"), EOSV_ERR_UNSUPPORTED;
+  if (B <= 0) return EOSV_OK;
+  const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
+  const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
+  const int ncb = ((Wq + 6) / 7 + CB_TILES - 1) / CB_TILES;
+  hipLaunchKernelGGL(stem_pool_x3_cb_kernel, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w, bias,
+                     (u16*)y, H, W, Hs, Ws, Hq, Wq);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
 }
 
 static bool stem_cb() {

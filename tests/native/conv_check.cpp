@@ -243,6 +243,82 @@ static int check_stem_pool(int N, int H, int W, bool direct = false) {
   return bad || rc ? 1 : 0;
 }
 
+
+// EOSV_F32X3 split-bf16 fused stem vs a double reference on the f32 operands: the kernel splits
+// frames and weights into bf16 hi + lo and drops lo.lo, so hi + lo of its output must be within
+// ~1e-4 relative of the exact value (the north star's f32 bound)
+static int check_stem_pool_x3(int N, int H, int W) {
+  const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
+  const int Hq = (Hs - 1) / 2 + 1, Wq = (Ws - 1) / 2 + 1;
+  unsigned s = 777;
+  std::vector<float> fr((size_t)N * 3 * H * W), wf(64 * 192, 0.f), b(64);
+  for (auto& v : fr) v = frand(s) * 2.f;
+  for (int o = 0; o < 64; ++o)
+    for (int kh = 0; kh < 7; ++kh)
+      for (int kw = 0; kw < 7; ++kw)
+        for (int c = 0; c < 3; ++c) wf[o * 192 + kh * 24 + kw * 3 + c] = frand(s) * 0.2f;
+  for (auto& v : b) v = frand(s) * 0.5f;
+  std::vector<unsigned short> w2(2 * 64 * 192);
+  for (int i = 0; i < 64 * 192; ++i) {
+    w2[i] = f2bf(wf[i]);
+    w2[64 * 192 + i] = f2bf(wf[i] - bf2f(w2[i]));
+  }
+  float *dfr, *db;
+  unsigned short *dw, *dy;
+  const size_t ny = (size_t)N * Hq * Wq * 192;
+  hipMalloc(&dfr, fr.size() * 4); hipMalloc(&dw, w2.size() * 2); hipMalloc(&dy, ny * 2); hipMalloc(&db, 64 * 4);
+  hipMemcpy(dfr, fr.data(), fr.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dw, w2.data(), w2.size() * 2, hipMemcpyHostToDevice);
+  hipMemcpy(db, b.data(), 64 * 4, hipMemcpyHostToDevice);
+  hipMemset(dy, 0xff, ny * 2);
+  const int rc = launch_stem_pool_x3(dfr, N, H, W, dw, db, dy, 0);
+  hipDeviceSynchronize();
+  std::vector<unsigned short> y(ny);
+  hipMemcpy(y.data(), dy, ny * 2, hipMemcpyDeviceToHost);
+  std::vector<double> st((size_t)Hs * Ws * 64);
+  long bad = 0;
+  double maxerr = 0, maxref = 0;
+  for (int n = 0; n < N; ++n) {
+    for (int sy = 0; sy < Hs; ++sy)
+      for (int sx = 0; sx < Ws; ++sx)
+        for (int o = 0; o < 64; ++o) {
+          double acc = b[o];
+          for (int kh = 0; kh < 7; ++kh)
+            for (int kw = 0; kw < 7; ++kw) {
+              const int iy = 2 * sy + kh - 3, ix = 2 * sx + kw - 3;
+              if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+              for (int c = 0; c < 3; ++c)
+                acc += (double)fr[(((size_t)n * 3 + c) * H + iy) * W + ix] * wf[o * 192 + kh * 24 + kw * 3 + c];
+            }
+          st[((size_t)sy * Ws + sx) * 64 + o] = acc > 0 ? acc : 0;
+        }
+    for (int py = 0; py < Hq; ++py)
+      for (int px = 0; px < Wq; ++px)
+        for (int o = 0; o < 64; ++o) {
+          double m = -INFINITY;
+          for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+              const int sy = 2 * py + dy, sx = 2 * px + dx;
+              if (sy >= 0 && sy < Hs && sx >= 0 && sx < Ws) m = fmax(m, st[((size_t)sy * Ws + sx) * 64 + o]);
+            }
+          const size_t base = (((size_t)n * Hq + py) * Wq + px) * 192 + o;
+          const double got = (double)bf2f(y[base]) + bf2f(y[base + 64]);
+          const bool dup = y[base + 128] == y[base];
+          const double e = fabs(got - m);
+          maxref = fmax(maxref, fabs(m));
+          if (e > 1e-4 * (1 + fabs(m)) || !dup) {
+            if (bad < 5) printf("  bad n%d py%d px%d o%d ref %f got %f dup %d\n", n, py, px, o, m, got, (int)dup);
+            ++bad;
+          }
+          maxerr = fmax(maxerr, e);
+        }
+  }
+  printf("%s stem_pool x3 N%d H%d W%d rc=%d maxerr %.3e (maxref %.3e) bad %ld\n", bad ? "FAIL" : "ok  ", N, H, W, rc,
+         maxerr, maxref, bad);
+  hipFree(dfr); hipFree(dw); hipFree(dy); hipFree(db);
+  return bad || rc ? 1 : 0;
+}
+
 // fused f32 stem + shift + ReLU + maxpool vs a double reference on the same f32 operands
 // (weights in the uploaded [64][176] = [kh 7][24] + 8 layout)
 static int check_stem_pool_f32(int N, int H, int W) {
@@ -321,6 +397,9 @@ int main() {
   if (stem_pool_bf16_ok(256, 256, true)) fails += check_stem_pool(2, 256, 256, true);  // (EOSV_STEM_CB=0: unfused)
   fails += check_stem_pool(3, 100, 88, true);
   fails += check_stem_pool(2, 60, 36, true);
+  fails += check_stem_pool_x3(2, 224, 224);
+  fails += check_stem_pool_x3(2, 256, 256);
+  fails += check_stem_pool_x3(3, 60, 36);
   fails += check_stem_pool_f32(2, 224, 224);
   fails += check_stem_pool_f32(3, 100, 86);
   fails += check_stem_pool_f32(2, 64, 48);
