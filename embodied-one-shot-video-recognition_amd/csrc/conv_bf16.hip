@@ -437,6 +437,12 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   // f32x3 (K tripled): 256x64 tiles for the Cout-64 stage-1 convs, +7 % over 128x64 (r01 A/B,
   // tools/ab_x3.sh)
   if (a.split && a.Cout <= 64 && v == 3) return launch_bf16<256, 64, 4, 1, false>(a, s);
+  // Cout 128 (ResNet stage 2, R50 bottleneck 1x1s, stride-2 entries and the fused downsample):
+  // 512x128 tiles (160 KiB, 8 waves of 128x64), the one-barrier-per-K-step loop of the 256x256
+  // tile.  r01 A/B (tools/ab_sets.sh): 12-15 % faster than the phased conv_bf16_p8 512x128 (whose 8
+  // barriers per K-tile cost more than its overlap gains: SQ MFMA-busy 0.29 vs 0.42) and 5 %
+  // faster than 128x128 on the stride-2 entry.
+  if ((v == 3 || v == 10) && a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
   if (v == 8 && a.Cout == 128) return launch_bf16<256, 128, 4, 2, false, 3>(a, s);  // 144 KiB, 1 block/CU
   if (v == 9 && a.Cout == 128) return launch_bf16<128, 128, 2, 2, false, 3>(a, s);  // 96 KiB
   if ((v == 3 || v == 8 || v == 9) && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);

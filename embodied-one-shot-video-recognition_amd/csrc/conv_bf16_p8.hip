@@ -473,7 +473,12 @@ bool conv_bf16_p8_ok(const ConvArgs& a) {
 // where the phased kernel is the default (r01 A/B on R18, tools/ab_env.sh EOSV_BF16_P8): the
 // stride-1 Cout = 128 convs (+1-3 %); at Cout >= 256 it ties conv_bf16_kernel's 256x256 tile and
 // on the stride-2 / 1x1 entries it is 5-10 % slower.  EOSV_BF16_P8=2 routes every eligible conv.
-bool conv_bf16_p8_default(const ConvArgs& a) { return a.Cout == 128 && a.stride == 1 && a.K >= 576; }
+// r01g: nowhere -- conv_bf16_kernel's 512x128 tile replaced it on the Cout = 128 convs (conv_bf16.hip);
+// EOSV_BF16_P8=2 still routes every eligible conv here for A/B
+bool conv_bf16_p8_default(const ConvArgs& a) {
+  (void)a;
+  return false;
+}
 // (with a fused downsample, a.K includes its Cin2 columns; the shape test above is unchanged)
 
 static int p8_env(const char* name, int dflt) {
