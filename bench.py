@@ -179,8 +179,8 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
            "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
                      f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
     if dtype == "f32x3":
-        out["kernel"] += ("; f32x3 = conv_bf16 kernels on the split (hi, lo, hi) layout + the exact-f32 "
-                          "stem, algorithmic (f32) FLOPs; peak = bf16 dense peak / 3")
+        out["kernel"] += ("; f32x3 = conv_bf16 kernels on the split (hi, lo, hi) layout + the split-bf16 fused "
+                          "stem (stem_pool_x3_cb_kernel), algorithmic (f32) FLOPs; peak = bf16 dense peak / 3")
     if args is not None and nl.sum() > 0:
         tr, src = measured_traffic(dtype, f"{args.arch}@{args.res}x{args.res}")
         out["traffic"] = tr

@@ -242,7 +242,7 @@ def test_full_size_c2_f32_bf16_agreement():
 @pytest.mark.parametrize("name,res", [("resnet18", 224), ("resnet50", 224), ("resnet18", 112)])
 def test_backbone_f32x3_vs_oracle(name, res):
     """EOSV_F32X3 (activations and weights as bf16 (hi, lo) pairs, every conv = the bf16 MFMA
-    products hi.hi + lo.hi + hi.lo in f32; exact-f32 stem): per-frame features within the north
+    products hi.hi + lo.hi + hi.lo in f32, the fused stem too): per-frame features within the north
     star's f32 tolerance, 1e-4 relative, of the f32 oracle.  A CPU simulation of the same
     arithmetic gave 4e-6 on R18 at 224 (plain bf16: 2e-3)."""
     sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)

@@ -44,7 +44,7 @@ for line in open(f"{src}/bench.log"):
 
 out = [f"# {tag} profile summary", "",
        "Command: `python bench.py --no-cpu-baseline` under `rocprofv3 --kernel-trace --stats` "
-       "(f32 primary + bf16 secondary legs); PMC passes `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
+       "(f32 primary + bf16 and f32x3 secondary legs); PMC passes `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` "
        "on `--steps 2` of the same command.", ""]
 if bench:
     rl = bench["roofline"]
@@ -54,10 +54,12 @@ if bench:
             f"- roofline: achieved {rl['achieved']} TF/s of {rl['peak']} ({rl['frac'] * 100:.1f} %), "
             f"end-to-end {rl.get('end_to_end_tflops')} TF/s",
             ]
-    if bench.get("secondary"):
-        s = bench["secondary"]
+    for key in [k for k in bench if k.startswith("secondary")]:
+        s = bench[key]
         out.append(f"- secondary {s['dtype']}: {s['value']} clips/s, roofline {s['roofline']['achieved']} TF/s "
-                   f"({s['roofline']['frac'] * 100:.1f} %), prediction agreement {s['prediction_agreement_vs_primary']}")
+                   f"({s['roofline']['frac'] * 100:.1f} % of {s['roofline']['peak']}), prediction agreement "
+                   f"{s['prediction_agreement_vs_primary']}, embeddings max rel vs primary "
+                   f"{s.get('embedding_max_rel_vs_primary')}")
     if bench.get("cpu_baseline"):
         cb = bench["cpu_baseline"]
         out.append(f"- cpu_baseline: {cb['value']} clips/s on {cb['cores']} cores ({cb['kind']})")
@@ -84,7 +86,14 @@ if bench:
     open(f"{dst}/{tag}_bench.json", "w").write(json.dumps(bench) + "\n")
 
 # conv-family HBM traffic per launch (read by bench.py into roofline.traffic)
-FAMILIES = {"f32": ("conv_f32",), "bf16": ("conv_bf16", "conv_rows_bf16", "stem_pool_bf16")}
+FAMILIES = {"f32": ("conv_f32",), "bf16": ("conv_bf16", "conv_rows_bf16", "stem_pool_bf16"),
+            "f32x3": ("conv_bf16", "stem_pool_x3")}
+
+
+def split_kernel(k):
+    """EOSV_F32X3 launches: the bf16 conv templates instantiated with SPLIT = true (their last
+    template argument) and the split-bf16 stem."""
+    return "stem_pool_x3" in k or (k.startswith("conv_bf16") and k.rstrip().endswith("true>"))
 traffic = {"source": f"profiles/{tag}_pmc_FETCH_SIZE.csv + profiles/{tag}_pmc_WRITE_SIZE.csv "
                      "(rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes of "
                      "`bench.py --no-cpu-baseline --steps 2`)",
@@ -94,7 +103,7 @@ for fam, keys in FAMILIES.items():
     tot = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
     n = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
     for k in pmc:
-        if any(key in k for key in keys):
+        if any(key in k for key in keys) and split_kernel(k) == (fam == "f32x3"):
             for c in tot:
                 tot[c] += pmc[k][c]
                 n[c] += cnt[k][c]
