@@ -186,7 +186,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
     // a.abl (profiling-only ablations, results wrong when set): 1 no main-loop loads,
-    // 4 no A loads, 8 no B loads, 2 no output stores, 16 no ds_reads, 32 no MFMAs, 64 no epilogue
+    // 4 no A loads, 8 no B loads, 16 no ds_reads, 32 no MFMAs, 64 no epilogue
     if (issue && !(a.abl & 1)) stage((kt + NS - 1) * BK, wslot, a.abl);
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
@@ -234,11 +234,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     asm volatile("" ::"v"(acc[0][0][0]));
     return;
   }
+  // The last K-step's vmcnt(0) is inline asm, invisible to the compiler: tell it, or it waits
+  // again (for the residual loads too) before the first LDS write below.
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
   u16* __restrict__ y = (u16*)a.y;
   const u16* __restrict__ res = (const u16*)a.res;
   // Epilogue staged through LDS (the ring is free now): pass i moves the i-th 32-row
   // M-subtile of every wave (WM*32 rows x BN cols, f32, rows padded by 4) so that the
   // residual loads and output stores are 16 B (8 bf16) per lane, whole 128-B lines.
+  // Output and residual go through buffer resources based at the tile's first row: rows past
+  // M lie beyond num_records and columns past Cout get an out-of-range offset, so such loads
+  // return 0 and such stores are dropped, without a branch.  Straight-line code lets the
+  // compiler count vmcnt exactly; the former per-chunk `if (m < M)` form made it wait
+  // vmcnt(0) -- for every earlier store -- before each residual use (r01g: the epilogue was
+  // 5-25 % of a layer).
   constexpr int EPR = WM * 32;   // rows per pass
   constexpr int EPS = BN + 4;    // f32 row stride
   static_assert(EPR * EPS * 4 <= NS * STAGE * 2, "epilogue tile must fit the ring");
@@ -254,35 +263,41 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int NPASS = BM / WM / 32;
   constexpr int IPT = EPR * (BN / 8) / (64 * NW);   // 16-B output chunks per thread per pass
   static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
-  // residual chunks of pass i, loaded one pass ahead (pass 0's right after the K-loop) so
-  // their latency overlaps the LDS staging instead of stalling each store
-  uint4 rv[2][IPT];
-  uint4 rl[2][SPLIT ? IPT : 1];  // SPLIT: the residual's lo block
   const long long ostr = SPLIT ? 3LL * a.Cout : a.Cout;  // output / residual pixel stride
-  auto chunk = [&](int i, int t, int& lrow, int& c8, long long& o) {
+  const long long tile_bytes = (long long)min(BM, M - m0) * ostr * 2;
+  const int nrec = (int)min(tile_bytes, 0x7fffffffLL);
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(y + (long long)m0 * ostr), (short)0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(res ? res + (long long)m0 * ostr : (const u16*)a.zero), (short)0, res ? nrec : 0, 0x00020000);
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  // v4u rv[2][IPT]: residual chunks of pass i, loaded one pass ahead (pass 0's right after the
+  // K-loop) so that their latency overlaps the LDS staging instead of stalling each store
+  v4u rv[2][IPT];
+  v4u rl[2][SPLIT ? IPT : 1];  // SPLIT: the residual's lo block
+  auto chunk = [&](int i, int t, int& lrow, int& c8, int& voff) {
     const int idx = tid + t * nthreads;
     lrow = idx / (BN / 8);
     c8 = idx - lrow * (BN / 8);
-    const int m = m0 + (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
+    const int ml = (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);  // row within the tile
     const int n = n0 + c8 * 8;
-    o = (m < M && n < a.Cout) ? (long long)m * ostr + n : -1;
+    voff = n < a.Cout ? (int)(((long long)ml * ostr + n) * 2) : (int)0x80000000;
   };
   auto load_res = [&](int i) {
 #pragma unroll
     for (int t = 0; t < IPT; ++t) {
-      int lrow, c8;
-      long long o;
-      chunk(i, t, lrow, c8, o);
-      if (o >= 0) {
-        rv[i & 1][t] = *(const uint4*)(res + o);
-        if constexpr (SPLIT) rl[i & 1][SPLIT ? t : 0] = *(const uint4*)(res + o + a.Cout);
-      }
+      int lrow, c8, voff;
+      chunk(i, t, lrow, c8, voff);
+      rv[i & 1][t] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, 0, 0);
+      if constexpr (SPLIT) rl[i & 1][SPLIT ? t : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff + 2 * a.Cout, 0, 0);
     }
   };
-  if (res) load_res(0);
+  // unconditional (no residual: rr has num_records 0, the loads return 0) and branch-free below
+  load_res(0);
+  const float rlow = a.relu ? 0.f : -INFINITY;  // ReLU as max(v, rlow)
 #pragma unroll
   for (int i = 0; i < NPASS; ++i) {
-    if (res && i + 1 < NPASS) load_res(i + 1);
+    if (i + 1 < NPASS) load_res(i + 1);
     // raw barriers in the epilogue: only the LDS staging needs ordering, and a
     // __syncthreads() fence would also wait for the residual prefetch and the stores
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -302,18 +317,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int t = 0; t < IPT; ++t) {
-      int lrow, c8;
-      long long o;
-      chunk(i, t, lrow, c8, o);
-      if (o < 0) continue;
+      int lrow, c8, voff;
+      chunk(i, t, lrow, c8, voff);
       const float4 v0 = *(const float4*)(ep + lrow * EPS + c8 * 8);
       const float4 v1 = *(const float4*)(ep + lrow * EPS + c8 * 8 + 4);
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (res) {
-        const uint4 r4 = rv[i & 1][t];
+      {
+        const v4u r4 = rv[i & 1][t];
         const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
         if constexpr (SPLIT) {
-          const uint4 l4 = rl[i & 1][SPLIT ? t : 0];
+          const v4u l4 = rl[i & 1][SPLIT ? t : 0];
           const unsigned rlo[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {  // hi + lo is exact in f32
@@ -328,27 +341,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
           }
         }
       }
-      unsigned pk[4], pl[4];
+      v4u pk, pl;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        float lo = v[2 * k], hi = v[2 * k + 1];
-        if (a.relu) {
-          lo = fmaxf(lo, 0.f);
-          hi = fmaxf(hi, 0.f);
-        }
+        const float lo = fmaxf(v[2 * k], rlow), hi = fmaxf(v[2 * k + 1], rlow);
         const u16 blo = f_to_bf(lo), bhi = f_to_bf(hi);
         pk[k] = (unsigned)blo | ((unsigned)bhi << 16);
         if constexpr (SPLIT)  // residual parts (exact differences)
           pl[k] = (unsigned)f_to_bf(lo - bf_to_f(blo)) | ((unsigned)f_to_bf(hi - bf_to_f(bhi)) << 16);
       }
-      if (a.abl & 2) {
-        asm volatile("" ::"v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]));
-      } else {
-        *(uint4*)(y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-        if constexpr (SPLIT) {
-          *(uint4*)(y + o + a.Cout) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
-          *(uint4*)(y + o + 2 * a.Cout) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-        }
+      __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff, 0, 0);
+      if constexpr (SPLIT) {
+        __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff + 4 * a.Cout, 0, 0);
       }
     }
   }
