@@ -325,10 +325,9 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
 
 // Column-blocked DIRECT variant (the default for W % 4 == 0): a workgroup of CB_TILES = 4 waves
 // owns the pooled columns 28c .. 28c + 27 of one image (c = blockIdx.y), so two workgroups share
-// a CU (54 KiB LDS, 226 VGPRs = 2 waves per SIMD) and one's MFMAs run while the other converts
-// rows, pools, stores and waits at its barriers.  The full-width workgroup (8 waves, 1 per CU)
-// serialised those: r01 ablations (EOSV_STEM_ABL) put its DMA + pool + barrier skeleton alone
-// at 0.64 ms and its MFMAs alone at ~0.6 ms of 1.70 ms per 3200 frames.  No width limit: the
+// a CU (54 KiB LDS, <= 256 VGPRs = 2 waves per SIMD).  That alone did not speed it up (r01g: the
+// SIMDs were issue-bound, ~290 VALU instructions per wave-step against 48 MFMAs); the VALU-lean
+// pool below did (1.56 -> 1.28 ms per 3200 frames).  No width limit: the
 // column blocks tile any W (ResNet-101 at 256 x 256 too).
 // Ring row of block c = padded-row bytes from 6 * pc0, pc0 = 28 * 4c - 2 (stem column 56c - 1
 // is its first: the left edge of pooled column 28c's window); a lane's k = its stem column
