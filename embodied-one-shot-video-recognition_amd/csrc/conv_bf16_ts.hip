@@ -1,0 +1,341 @@
+// Tap-shift implicit GEMM for the stride-1 3x3 convs on bf16 MFMA (ResNet stages 2-4 and the
+// R50 bottleneck 3x3s; bf16 and the EOSV_F32X3 split layout).
+//
+// conv_bf16_kernel stages one im2col A row per output pixel per tap, so every input pixel
+// crosses L2 -> LDS 9 times, and its LDS-DMA feed (not the MFMA pipe) bounds it (DESIGN.md
+// section 3).  Here a stage is (32-channel slice, kernel row kh): the A tile holds the input
+// row oh + kh - 1 of the BM + 2 consecutive output pixels m0 - 1 .. m0 + BM (each at its own
+// column), and the three taps kw = 0, 1, 2 of that kernel row read it at row offsets 0, 1, 2:
+// output pixel m0 + r at tap kw needs input column ow + kw - 1, which is where pixel
+// m0 + r + kw - 1 sits -- unless ow + kw - 1 leaves the row, and those A fragments (ow = 0 at
+// kw = 0, ow = W - 1 at kw = 2: the conv's zero padding) are zeroed in registers.  A is staged
+// once per kernel row instead of once per tap (3x fewer A bytes); B holds the 3 taps' weights.
+//
+// Staged bytes per stage, 512 x 128 tile: A 528 x 64 B + B 3 x 128 x 64 B = 58 KiB for
+// 12.6 MFLOP (216 FLOP/B; the im2col tile: 105); 256 x 256: 65 KiB for 12.6 MFLOP (194; was 128).
+// LDS rows are 64 B (BK = 32: one v_mfma_f32_16x16x32_bf16 k-step); 16-B chunk c of row R sits
+// at c ^ ((R >> 1) & 3), applied on the DMA source: conflict-free ds_read_b128 for the fragment
+// rows at any row offset (checked for every base offset against the b128 lane groups of
+// MI355X_MICROARCH.md, LDS).  Ring, barriers and epilogue as conv_bf16_kernel.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+
+namespace eosv {
+
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)v << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
+__device__ __forceinline__ void dma16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+}  // namespace
+
+template <int BM, int BN, int WM, int WN, bool SPLIT>
+__global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) {
+  constexpr int BK = 32;                        // channels per stage
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  constexpr int AR = (BM + 2 + 15) / 16 * 16;   // staged A rows (output pixels m0 - 1 .. m0 + BM)
+  constexpr int AP = AR / 16;                   // A DMA pieces (16 rows x 64 B = 1 KiB)
+  constexpr int APW = (AP + NW - 1) / NW;       // A pieces per wave (the last ones partial)
+  constexpr int BP = 3 * BN / 16;               // B DMA pieces (3 taps x BN rows)
+  static_assert(BP % NW == 0, "B pieces divide over the waves");
+  constexpr int BPW = BP / NW;
+  constexpr int STAGE = (AR + 3 * BN) * BK;     // bf16 elements per ring slot
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nN = a.Cout / BN;
+  const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
+  const int mt = bt / nN;
+  const int nt = bt - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const u16* __restrict__ x = (const u16*)a.x;
+  const u16* __restrict__ w = (const u16*)a.w;
+  const u16* zero = (const u16*)a.zero;
+
+  // A pieces: lane -> staged row 16 * piece + (lane >> 2), LDS chunk slot lane & 3 (source chunk
+  // slot ^ swizzle); apix = the row's pixel at its own position, amask bit kh = input row
+  // oh + kh - 1 inside the image
+  const int lr = lane >> 2, sl = lane & 3;
+  const u16* apix[APW];
+  unsigned amask[APW];
+#pragma unroll
+  for (int t = 0; t < APW; ++t) {
+    const int piece = wid + NW * t;
+    const int row = piece * 16 + lr;
+    const int p = m0 - 1 + row;
+    apix[t] = zero;
+    amask[t] = 0;
+    if (piece < AP && row <= BM + 1 && p >= 0 && p < M) {
+      const int rem = p % HW;
+      const int oh = rem / a.W;
+      apix[t] = x + (long long)p * a.Cin + (sl ^ ((row >> 1) & 3)) * 8;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+        if ((unsigned)(oh + kh - 1) < (unsigned)a.H) amask[t] |= 1u << kh;
+    }
+  }
+  // DS (fused 1x1 downsample, ConvArgs::x2): the same rows' pixels in x2 at (oh s2, ow s2);
+  // staged rows 1 .. BM only (a DS stage is read at tap offset 1)
+  const u16* apix2[APW];
+  const u16* x2 = (const u16*)a.x2;
+#pragma unroll
+  for (int t = 0; t < APW; ++t) {
+    const int piece = wid + NW * t;
+    const int row = piece * 16 + lr;
+    const int p = m0 - 1 + row;
+    apix2[t] = zero;
+    if (x2 && piece < AP && row >= 1 && row <= BM && p < M) {
+      const int img = p / HW, rem = p - img * HW;
+      const int oh = rem / a.W, ow = rem - oh * a.W;
+      apix2[t] = x2 + (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 +
+                 (sl ^ ((row >> 1) & 3)) * 8;
+    }
+  }
+  // B pieces: staged row kw * BN + (output channel - n0)
+  const u16* bsrc[BPW];
+  int btap[BPW];
+#pragma unroll
+  for (int t = 0; t < BPW; ++t) {
+    const int row = (wid + NW * t) * 16 + lr;
+    const int kw = row / BN;
+    btap[t] = kw;
+    bsrc[t] = w + (long long)(n0 + row - kw * BN) * a.K + (sl ^ ((row >> 1) & 3)) * 8;
+  }
+  const long long rowoff = (long long)a.W * a.Cin;  // elements from input row oh to oh + 1
+  auto kidx = [&](int kh, int kw, int c) -> int {   // K column of tap (kh, kw), channel c (32-aligned)
+    return a.kcm ? (((c >> 6) * 9 + kh * 3 + kw) << 6) + (c & 63) : (kh * 3 + kw) * a.Cin + c;
+  };
+  const int nst3 = 3 * (a.Cin / BK);  // 3x3 stages; then Cin2 / BK fused-downsample stages
+  auto stage = [&](int st, int slot) {
+    u16* As = smem + slot * STAGE;
+    u16* Bs = As + AR * BK;
+    if (st >= nst3) {  // DS stage: A = x2 pixels, B = the 1x1 weights (K columns K1 + c) in tap slot 1
+      const int c0 = (st - nst3) * BK;
+#pragma unroll
+      for (int t = 0; t < APW; ++t) {
+        const int piece = wid + NW * t;
+        if (piece < AP) dma16(apix2[t] + (apix2[t] != zero ? c0 : 0), As + piece * 16 * BK);
+      }
+#pragma unroll
+      for (int t = 0; t < BPW; ++t)
+        if (btap[t] == 1) dma16(bsrc[t] + a.K1 + c0, Bs + (wid + NW * t) * 16 * BK);
+      return;
+    }
+    const int cs = st / 3, kh = st - 3 * cs, c0 = cs * BK;
+    const long long aoff = (long long)(kh - 1) * rowoff + c0;
+#pragma unroll
+    for (int t = 0; t < APW; ++t) {
+      const int piece = wid + NW * t;
+      if (piece < AP) {
+        const u16* src = ((amask[t] >> kh) & 1) ? apix[t] + aoff : zero;
+        dma16(src, As + piece * 16 * BK);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < BPW; ++t) dma16(bsrc[t] + kidx(kh, btap[t], c0), Bs + (wid + NW * t) * 16 * BK);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r = lane & 15;
+  const int q = lane >> 4;
+  // image-column edges of this lane's output rows: bit 2i = ow 0 (tap kw 0 reads padding),
+  // bit 2i + 1 = ow W - 1 (kw 2)
+  unsigned emask = 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / WM) + i * 16 + r;
+    const int ow = (m % HW) % a.W;
+    if (ow == 0) emask |= 1u << (2 * i);
+    if (ow == a.W - 1) emask |= 2u << (2 * i);
+  }
+
+  const int nst = nst3 + (x2 ? a.Cin2 / BK : 0);
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) stage(st + 1, cur ^ 1);
+    const u16* As = smem + cur * STAGE;
+    const u16* Bs = As + AR * BK;
+    const bool ds = st >= nst3;  // a DS stage is read at offset 1 only (no taps, no edges)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      if (ds && kw != 1) continue;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / WM) + i * 16 + r + kw;  // pixel m0 + (row - kw) at tap kw
+        af[i] = *(const bf16x8*)(As + row * BK + ((q ^ ((row >> 1) & 3)) * 8));
+        if (kw != 1 && ((emask >> (2 * i + (kw >> 1))) & 1)) af[i] = bf16x8{};  // (never in a DS stage)
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = kw * BN + wn * (BN / WN) + j * 16 + r;
+        bfr[j] = *(const bf16x8*)(Bs + row * BK + ((q ^ ((row >> 1) & 3)) * 8));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // Epilogue as conv_bf16_kernel's (LDS-staged 16-B rows, buffer resources, branch-free)
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the asm waits above are invisible to the compiler
+  u16* __restrict__ y = (u16*)a.y;
+  const u16* __restrict__ res = (const u16*)a.res;
+  constexpr int EPR = WM * 32;
+  constexpr int EPS = BN + 4;
+  static_assert(EPR * EPS * 4 <= 2 * STAGE * 2, "epilogue tile must fit the ring");
+  float* ep = (float*)smem;
+  float bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 16 + r;
+    bcol[j] = a.bias ? a.bias[n] : 0.f;
+  }
+  const int nthreads = 64 * NW;
+  constexpr int NPASS = BM / WM / 32;
+  constexpr int IPT = EPR * (BN / 8) / (64 * NW);
+  static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
+  const long long ostr = SPLIT ? 3LL * a.Cout : a.Cout;
+  const long long tile_bytes = (long long)min(BM, M - m0) * ostr * 2;
+  const int nrec = (int)min(tile_bytes, 0x7fffffffLL);
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(y + (long long)m0 * ostr), (short)0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(res ? res + (long long)m0 * ostr : zero), (short)0, res ? nrec : 0, 0x00020000);
+  v4u rv[2][IPT];
+  v4u rl[2][SPLIT ? IPT : 1];
+  auto chunk = [&](int i, int t, int& lrow, int& c8, int& voff) {
+    const int idx = tid + t * nthreads;
+    lrow = idx / (BN / 8);
+    c8 = idx - lrow * (BN / 8);
+    const int ml = (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
+    voff = (int)(((long long)ml * ostr + n0 + c8 * 8) * 2);
+  };
+  auto load_res = [&](int i) {
+#pragma unroll
+    for (int t = 0; t < IPT; ++t) {
+      int lrow, c8, voff;
+      chunk(i, t, lrow, c8, voff);
+      rv[i & 1][t] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, 0, 0);
+      if constexpr (SPLIT) rl[i & 1][SPLIT ? t : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff + 2 * a.Cout, 0, 0);
+    }
+  };
+  load_res(0);
+  const float rlow = a.relu ? 0.f : -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NPASS; ++i) {
+    if (i + 1 < NPASS) load_res(i + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lrow = wm * 32 + t * 16 + 4 * q + e;  // 16x16 C/D map: row 4(lane/16) + e
+          ep[lrow * EPS + wn * (BN / WN) + j * 16 + r] = acc[i * 2 + t][j][e] + bcol[j];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int t = 0; t < IPT; ++t) {
+      int lrow, c8, voff;
+      chunk(i, t, lrow, c8, voff);
+      const float4 v0 = *(const float4*)(ep + lrow * EPS + c8 * 8);
+      const float4 v1 = *(const float4*)(ep + lrow * EPS + c8 * 8 + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      const v4u r4 = rv[i & 1][t];
+      const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
+      if constexpr (SPLIT) {
+        const v4u l4 = rl[i & 1][SPLIT ? t : 0];
+        const unsigned rlo[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // hi + lo is exact in f32
+          v[2 * k] += bf2f((u16)(ru[k] & 0xffff)) + bf2f((u16)(rlo[k] & 0xffff));
+          v[2 * k + 1] += bf2f((u16)(ru[k] >> 16)) + bf2f((u16)(rlo[k] >> 16));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += bf2f((u16)(ru[k] & 0xffff));
+          v[2 * k + 1] += bf2f((u16)(ru[k] >> 16));
+        }
+      }
+      v4u pk, pl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = fmaxf(v[2 * k], rlow), hi = fmaxf(v[2 * k + 1], rlow);
+        const u16 blo = f2bf(lo), bhi = f2bf(hi);
+        pk[k] = (unsigned)blo | ((unsigned)bhi << 16);
+        if constexpr (SPLIT)
+          pl[k] = (unsigned)f2bf(lo - bf2f(blo)) | ((unsigned)f2bf(hi - bf2f(bhi)) << 16);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff, 0, 0);
+      if constexpr (SPLIT) {
+        __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff + 4 * a.Cout, 0, 0);
+      }
+    }
+  }
+}
+
+// shapes this kernel takes: stride-1 pad-1 3x3, Cin % 32, Cout 128 (512 x 128 tiles) or a
+// multiple of 256 (256 x 256), optionally a fused 1x1 downsample (Cin2 % 32), no stem
+bool conv_bf16_ts_ok(const ConvArgs& a) {
+  const bool ds_ok = !a.x2 ? a.K == 9 * a.Cin : (a.K1 == 9 * a.Cin && a.K == a.K1 + a.Cin2 && a.Cin2 % 32 == 0);
+  return a.Cin != 3 && a.KH == 3 && a.KW == 3 && a.KWp == 3 && a.stride == 1 && a.pad == 1 && a.Ho == a.H &&
+         a.Wo == a.W && a.Cin % 32 == 0 && ds_ok && (a.Cout == 128 || a.Cout % 256 == 0) && a.zero;
+}
+
+int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
+  if (!conv_bf16_ts_ok(a)) return set_error("conv_bf16_ts: unsupported shape"), EOSV_ERR_UNSUPPORTED;
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  const int BM = a.Cout == 128 ? 512 : 256, BN = a.Cout == 128 ? 128 : 256;
+  const long long nb = ((M + BM - 1) / BM) * (a.Cout / BN);
+  if (nb > 0x7fffffffLL) return set_error("conv_bf16_ts: grid too large"), EOSV_ERR_UNSUPPORTED;
+#define TS_LAUNCH(BM_, BN_, WM_, WN_)                                                                             \
+  if (a.split)                                                                                                   \
+    hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, true>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), 0, \
+                       s, a);                                                                                    \
+  else                                                                                                           \
+    hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, false>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), \
+                       0, s, a);
+  if (a.Cout == 128) {
+    TS_LAUNCH(512, 128, 4, 2)
+  } else {
+    TS_LAUNCH(256, 256, 2, 4)
+  }
+#undef TS_LAUNCH
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+}  // namespace eosv
