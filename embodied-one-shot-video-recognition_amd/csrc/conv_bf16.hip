@@ -435,13 +435,15 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
-  // tap-shift kernel (conv_bf16_ts.hip) for the stride-1 3x3 convs with Cout = 128 (r01g A/B: 3-12 %
-  // faster; at Cout >= 256 its 64-B rows lost 2-8 % to the 256x256 im2col tile)
+  // tap-shift kernel (conv_bf16_ts.hip) for the stride-1 3x3 convs with Cout = 128 (r01g A/B: 5-6 %
+  // faster) and the f32x3 Cout = 64 convs (512x64: 10-12 % faster than 256x64); at Cout >= 256
+  // its 64-B rows lost 2-8 % to the 256x256 im2col tile
   static const int ts = [] {
-    const char* e = getenv("EOSV_BF16_TS");  // 0 never, 1 Cout 128, 2 every eligible shape (A/B switch)
+    const char* e = getenv("EOSV_BF16_TS");  // 0 never, 1 default shapes, 2 every eligible shape (A/B switch)
     return e ? atoi(e) : 1;
   }();
-  if (ts && conv_bf16_ts_ok(a) && (ts == 2 || a.Cout == 128)) return launch_conv_bf16_ts(a, s);
+  if (ts && conv_bf16_ts_ok(a) && (ts == 2 || a.Cout == 128 || (a.Cout == 64 && a.split)))
+    return launch_conv_bf16_ts(a, s);
   if (bf16_p8() && conv_bf16_p8_ok(a) && (bf16_p8() == 2 || conv_bf16_p8_default(a))) return launch_conv_bf16_p8(a, s);
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
   // K = 64 1x1 convs all measured slower than this choice

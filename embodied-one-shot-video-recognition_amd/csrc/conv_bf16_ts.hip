@@ -46,8 +46,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   constexpr int AP = AR / 16;                   // A DMA pieces (16 rows x 64 B = 1 KiB)
   constexpr int APW = (AP + NW - 1) / NW;       // A pieces per wave (the last ones partial)
   constexpr int BP = 3 * BN / 16;               // B DMA pieces (3 taps x BN rows)
-  static_assert(BP % NW == 0, "B pieces divide over the waves");
-  constexpr int BPW = BP / NW;
+  constexpr int BPW = (BP + NW - 1) / NW;       // B pieces per wave (the last ones partial)
   constexpr int STAGE = (AR + 3 * BN) * BK;     // bf16 elements per ring slot
   __shared__ __attribute__((aligned(16))) u16 smem[2 * STAGE];
 
@@ -110,7 +109,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   int btap[BPW];
 #pragma unroll
   for (int t = 0; t < BPW; ++t) {
-    const int row = (wid + NW * t) * 16 + lr;
+    const int row = min((wid + NW * t) * 16, BP * 16 - 16) + lr;  // pieces past BP: never issued
     const int kw = row / BN;
     btap[t] = kw;
     bsrc[t] = w + (long long)(n0 + row - kw * BN) * a.K + (sl ^ ((row >> 1) & 3)) * 8;
@@ -132,7 +131,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
       }
 #pragma unroll
       for (int t = 0; t < BPW; ++t)
-        if (btap[t] == 1) dma16(bsrc[t] + a.K1 + c0, Bs + (wid + NW * t) * 16 * BK);
+        if (wid + NW * t < BP && btap[t] == 1) dma16(bsrc[t] + a.K1 + c0, Bs + (wid + NW * t) * 16 * BK);
       return;
     }
     const int cs = st / 3, kh = st - 3 * cs, c0 = cs * BK;
@@ -146,7 +145,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
       }
     }
 #pragma unroll
-    for (int t = 0; t < BPW; ++t) dma16(bsrc[t] + kidx(kh, btap[t], c0), Bs + (wid + NW * t) * 16 * BK);
+    for (int t = 0; t < BPW; ++t)
+      if (wid + NW * t < BP) dma16(bsrc[t] + kidx(kh, btap[t], c0), Bs + (wid + NW * t) * 16 * BK);
   };
 
   f32x4 acc[TM][TN];
@@ -307,18 +307,18 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   }
 }
 
-// shapes this kernel takes: stride-1 pad-1 3x3, Cin % 32, Cout 128 (512 x 128 tiles) or a
-// multiple of 256 (256 x 256), optionally a fused 1x1 downsample (Cin2 % 32), no stem
+// shapes this kernel takes: stride-1 pad-1 3x3, Cin % 32, Cout 64 (512 x 64 tiles), 128 (512 x 128)
+// or a multiple of 256 (256 x 256), optionally a fused 1x1 downsample (Cin2 % 32), no stem
 bool conv_bf16_ts_ok(const ConvArgs& a) {
   const bool ds_ok = !a.x2 ? a.K == 9 * a.Cin : (a.K1 == 9 * a.Cin && a.K == a.K1 + a.Cin2 && a.Cin2 % 32 == 0);
   return a.Cin != 3 && a.KH == 3 && a.KW == 3 && a.KWp == 3 && a.stride == 1 && a.pad == 1 && a.Ho == a.H &&
-         a.Wo == a.W && a.Cin % 32 == 0 && ds_ok && (a.Cout == 128 || a.Cout % 256 == 0) && a.zero;
+         a.Wo == a.W && a.Cin % 32 == 0 && ds_ok && (a.Cout == 64 || a.Cout == 128 || a.Cout % 256 == 0) && a.zero;
 }
 
 int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   if (!conv_bf16_ts_ok(a)) return set_error("conv_bf16_ts: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   const long long M = (long long)a.N * a.Ho * a.Wo;
-  const int BM = a.Cout == 128 ? 512 : 256, BN = a.Cout == 128 ? 128 : 256;
+  const int BM = a.Cout <= 128 ? 512 : 256, BN = a.Cout <= 128 ? a.Cout : 256;
   const long long nb = ((M + BM - 1) / BM) * (a.Cout / BN);
   if (nb > 0x7fffffffLL) return set_error("conv_bf16_ts: grid too large"), EOSV_ERR_UNSUPPORTED;
 #define TS_LAUNCH(BM_, BN_, WM_, WN_)                                                                             \
@@ -328,7 +328,9 @@ int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   else                                                                                                           \
     hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, false>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), \
                        0, s, a);
-  if (a.Cout == 128) {
+  if (a.Cout == 64) {
+    TS_LAUNCH(512, 64, 8, 1)
+  } else if (a.Cout == 128) {
     TS_LAUNCH(512, 128, 4, 2)
   } else {
     TS_LAUNCH(256, 256, 2, 4)
