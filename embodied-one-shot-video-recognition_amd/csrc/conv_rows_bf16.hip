@@ -141,7 +141,10 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
   for (int k = 0; strip < nstrips; ++k, strip += gridDim.x) {
     const int cur = k & 1;
     const int next = strip + gridDim.x;
-    if (next < nstrips) stage(next, cur ^ 1);
+    // a.abl (EOSV_CONV_ABL, profiling-only, results wrong): 1 no prefetch DMA, 2 no residual
+    // loads, 16 no ds_reads, 32 no MFMAs, 64 no epilogue stores
+    const int abl = a.abl;
+    if (next < nstrips && !(abl & 1)) stage(next, cur ^ 1);
     const u16* Ib = In + cur * IN_ELEMS;
     const int img = strip / spi;
     const int y0 = (strip - img * spi) * TR;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     // loads: with an LDS-DMA in flight hipcc waits vmcnt(0) before every use of an ordinary
     // load's result (and here even before issuing one), which would drain the prefetch.
     uint2 rv[2][4];
-    if (res) {
+    if (res && !(abl & 2)) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -170,10 +173,11 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     // next step's 6 ds_reads are issued (inline asm, so hipcc can neither sink them next to
     // their MFMAs nor wait lgkmcnt(0) per read) ahead of this step's 8 MFMAs, and one
     // lgkmcnt(0) per step retires them; sched_barrier keeps each step's MFMAs inside it.
-    bf16x8 af[2][2], bf[2][4];
+    bf16x8 af[2][2] = {}, bf[2][4] = {};
     auto frags = [&](int t, int b) {
       const int tap = t >> 1, dy = tap / 3, dx = tap - (tap / 3) * 3;
       const int lc = 4 * (t & 1) + q;  // this lane's 16-B chunk of the 32-deep k-slice
+      if (abl & 16) return;
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
         const int pix = apix[mi] + dy * SLOTS + dx;
@@ -192,11 +196,12 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     for (int t = 0; t < 18; ++t) {
       if (t + 1 < 18) frags(t + 1, (t + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);  // the reads go out before this step's MFMAs
+      if (!(abl & 32))
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[t & 1][j], af[t & 1][mi], acc[mi][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j)
+            acc[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[t & 1][j], af[t & 1][mi], acc[mi][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // ... and the wait after all of them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -227,8 +232,9 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
         const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-        *(uint2*)(y + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q) = make_uint2(lo, hi);
+        if (!(abl & 64)) *(uint2*)(y + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q) = make_uint2(lo, hi);
       }
+    if (abl & 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // next strip's DMA (issued before this strip's 8 stores per lane) must have landed, and
     // every wave's reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
