@@ -62,6 +62,7 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
 }
 }  // namespace
 
+template <bool ABL>
 __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstrips) {
   __shared__ __attribute__((aligned(16))) u16 smem[W_ELEMS + 2 * IN_ELEMS];
   u16* Ws = smem;
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     const int next = strip + gridDim.x;
     // a.abl (EOSV_CONV_ABL, profiling-only, results wrong): 1 no prefetch DMA, 2 no residual
     // loads, 16 no ds_reads, 32 no MFMAs, 64 no epilogue stores
-    const int abl = a.abl;
+    const int abl = ABL ? a.abl : 0;  // the default instance compiles without the ablation branches
     if (next < nstrips && !(abl & 1)) stage(next, cur ^ 1);
     const u16* Ib = In + cur * IN_ELEMS;
     const int img = strip / spi;
@@ -260,7 +261,10 @@ int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s) {
   if (nstrips <= 0) return EOSV_OK;
   if (nstrips > 0x7fffffffLL) return set_error("conv_rows: too many strips"), EOSV_ERR_UNSUPPORTED;
   const unsigned grid = (unsigned)std::min<long long>(nstrips, ncu);
-  hipLaunchKernelGGL(conv_rows_bf16_kernel, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
+  if (a.abl)
+    hipLaunchKernelGGL(conv_rows_bf16_kernel<true>, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
+  else
+    hipLaunchKernelGGL(conv_rows_bf16_kernel<false>, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
