@@ -237,6 +237,22 @@ def normalize_frames(rgb: torch.Tensor, crop: int = 224, mean=IMAGENET_MEAN, std
     return out
 
 
+def crop_normalize_frames(rgb: torch.Tensor, crop: int, top: int, left: int, flip: bool = False,
+                          mean=IMAGENET_MEAN, std=IMAGENET_STD, stream=None) -> torch.Tensor:
+    """Decoded uint8 frames [F,H,W,3] (device) -> window (top, left, crop) [mirrored] -> normalised
+    [F,3,crop,crop] f32 (utils.py:57-91: ClipRandomCrop / CenterCrop, hflip, ToTensor, Normalize)."""
+    _require_cuda(rgb, "rgb", torch.uint8)
+    F, H, W, C = rgb.shape
+    if C != 3:
+        raise ValueError("rgb must be [F,H,W,3]")
+    out = torch.empty(F, 3, crop, crop, device=rgb.device, dtype=torch.float32)
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    sd = (ctypes.c_float * 3)(*[float(v) for v in std])
+    check(lib().eosv_crop_normalize_frames(ptr(rgb), F, H, W, crop, int(top), int(left), int(bool(flip)), m, sd,
+                                           ptr(out), stream_ptr(stream)), "eosv_crop_normalize_frames")
+    return out
+
+
 def synth_frames(params: np.ndarray, H: int, W: int, device=None, out: Optional[torch.Tensor] = None,
                  stream=None) -> torch.Tensor:
     """Generate frames [F,3,H,W] on the device from a [F,4] u64 table (see frame_table)."""

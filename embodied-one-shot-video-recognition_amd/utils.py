@@ -67,19 +67,30 @@ def transfer_weights(model_from, model_to):
 
 
 def transforms(mode):
-    """utils.py:80-91: PIL image -> normalised [3,224,224] tensor (centre crop in test mode)."""
-    src = _frames.JpegFrames('', crop=IMG_crop_size[0], init_h=IMG_INIT_H)
+    """utils.py:80-91: PIL image -> normalised [3,224,224] tensor on the GPU
+    (eosv_crop_normalize_frames).  test/val: centre crop.  train: one random window and flip
+    per transform object, as ClipRandomCrop / ClipRandomHorizontalFlip (utils.py:57-78)."""
+    import random as _rnd
+    from eosv import engine as _engine
+
+    c = IMG_crop_size[0]
+    flip = _rnd.random() < 0.5 if mode == 'train' else False
+    state = {}
 
     def apply(img):
         a = np.asarray(img.convert('RGB'))
         h, w = a.shape[:2]
-        c = IMG_crop_size[0]
-        i, j = int(round((h - c) / 2.0)), int(round((w - c) / 2.0))
-        x = a[i:i + c, j:j + c].astype(np.float32) / np.float32(255.0)
-        x = (x - _frames.MEAN) / _frames.STD
-        return torch.from_numpy(np.ascontiguousarray(x.transpose(2, 0, 1)))
+        if mode == 'train':
+            if 'ij' not in state:
+                state['ij'] = (0, 0) if (h == c and w == c) else (
+                    int(torch.randint(0, h - c + 1, size=(1,)).item()),
+                    int(torch.randint(0, w - c + 1, size=(1,)).item()))
+            i, j = state['ij']
+        else:
+            i, j = int(round((h - c) / 2.0)), int(round((w - c) / 2.0))
+        rgb = torch.from_numpy(np.array(a)[None]).cuda()
+        return _engine.crop_normalize_frames(rgb, c, i, j, flip)[0]
 
-    apply.source = src
     return apply
 
 
@@ -115,7 +126,7 @@ def get_video_from_video_info_2(video_info, mode, video_frames=VIDEO_FRAMES, fra
     ids = _frames.clip_frame_ids(n_all, video_frames, mode)
     fd = KINETICS_FRAME_DIR if frame_dir is None else frame_dir
     paths = [os.path.join(fd, video_info, 'image_%05d.jpg' % f) for f in ids]
-    return torch.from_numpy(src.frames(video_info, ids, mode)), np.array(paths)
+    return src.frames_tensor(video_info, ids, mode), np.array(paths)
 
 
 def get_video_from_video_info_3(video_info, mode, video_frames=VIDEO_FRAMES, frame_dir=None):

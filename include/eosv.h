@@ -130,6 +130,12 @@ int eosv_temporal_smooth(const float* d_x, int rows, int cols, float lamda1, flo
 int eosv_normalize_frames(const uint8_t* d_rgb, int n_frames, int H, int W, int crop, const float* mean,
                           const float* std, float* d_out, eosv_stream_t stream);
 
+/* Same transform with an explicit window (utils.py:57-78 ClipRandomCrop + ClipRandomHorizontalFlip,
+ * train mode): rows top .. top+crop-1, columns left .. left+crop-1, mirrored when flip != 0.
+ * The window must lie inside H x W. */
+int eosv_crop_normalize_frames(const uint8_t* d_rgb, int n_frames, int H, int W, int crop, int top, int left,
+                               int flip, const float* mean, const float* std, float* d_out, eosv_stream_t stream);
+
 /* Deterministic synthetic frames, bit-identical to eosv/synth.py:synth_frame.
  * For frame f: class seed, video seed, noise seed (u64) and frame id in d_params
  * [n_frames, 4] (u64); writes d_frames [n_frames,3,H,W] f32 NCHW.  Frames with
