@@ -128,13 +128,14 @@ class TestNetwork():
                     rows.append((cs, vs, _synth.mix64_int(((crc << 20) + f) ^ _synth.TAG_NOISE), f))
                 rows += [(0, 0, 0, 0)] * (pad_to - len(ids))
             return _engine.synth_frames(np.array(rows, np.uint64).reshape(-1, 4), H, W, dev)
+        # real frames: JPEG decode on the host, crop + normalise on the GPU (eosv/frames.py)
         out = []
         for vi, ids, pad_to in clips:
-            v = torch.from_numpy(src.frames(vi, ids, 'test'))
+            v = src.frames_tensor(vi, ids, 'test').to(dev)
             if pad_to > len(ids):
-                v = torch.cat([v, torch.zeros(pad_to - len(ids), 3, H, W)])
+                v = torch.cat([v, torch.zeros(pad_to - len(ids), 3, H, W, device=v.device)])
             out.append(v)
-        return torch.cat(out).to(dev)
+        return torch.cat(out)
 
     def _ids(self, vi, mode):
         n_all = utils.frame_source().frame_count(vi)
@@ -181,8 +182,8 @@ class TestNetwork():
         preds = []
         for b0 in range(0, len(mine), self.episodes_per_batch):
             preds += self._baseline_batch([plans[e] for e in mine[b0:b0 + self.episodes_per_batch]])
-        accs, _ = self._gather(mine, preds, n, [p['query_y'] for p in plans])
-        self.last_accs = accs
+        accs, all_preds = self._gather(mine, preds, n, [p['query_y'] for p in plans])
+        self.last_accs, self.last_preds = accs, all_preds
         if rank == 0:
             return self._write_results(accs)
 

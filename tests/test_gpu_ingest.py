@@ -91,3 +91,68 @@ def test_transforms_dropin(frame_dir):
     x = a[i:i + 224, j:j + 224].astype(np.float32) / np.float32(255.0)
     ref = ((x - frames_ref.MEAN) / frames_ref.STD).transpose(2, 0, 1)
     assert out.is_cuda and np.array_equal(out.cpu().numpy().view(np.uint32), np.ascontiguousarray(ref).view(np.uint32))
+
+
+# end-to-end: 6 classes x 2 videos (5-way 1-shot needs k_shot + 1 = 2 videos of the query class)
+E2E = [(f"c{c}/v{v}", 320 if (c + v) % 3 else 200, 240 if (c + v) % 3 else 150, 30 if v else 18)
+       for c in range(6) for v in range(2)]
+E2E[3] = ("c1/v1", 320, 240, 10)  # short clip: zero-padded support / truncated query
+
+
+@pytest.fixture(scope="module")
+def e2e_dir(tmp_path_factory):
+    from PIL import Image
+
+    root = tmp_path_factory.mktemp("e2e")
+    rng = np.random.default_rng(12)
+    for vi, w, h, n in E2E:
+        d = root / vi
+        d.mkdir(parents=True)
+        cls = np.random.default_rng(int(vi[1])).integers(0, 256, size=(h, w, 3))
+        for f in range(1, n + 1):
+            a = np.clip(cls + rng.integers(-60, 61, size=(h, w, 3)), 0, 255).astype(np.uint8)
+            Image.fromarray(a).save(d / ("image_%05d.jpg" % f), quality=90)
+        (d / "extra.txt").write_text("x")
+    (root / "test.list").write_text("".join(vi + "\n" for vi, *_ in E2E))
+    return str(root)
+
+
+def test_network_baseline_on_jpeg_frames(e2e_dir, tmp_path, monkeypatch):
+    """TestNetwork.test_network_baseline over real JPEG clips (batched GPU path: host decode,
+    GPU ingest, backbone, clip embedding, protonet) == the reference's per-episode loop restated
+    on the CPU (oracle: frames_ref loaders + torch-CPU ResNet-18 + classifier restatement):
+    integer predictions bit-exact."""
+    import os
+
+    import network_test
+    import utils
+    from eosv import arch, synth
+    from oracle import harness_ref, resnet_ref
+
+    n_ep = 4
+    monkeypatch.setattr(utils, "TEST_LIST", os.path.join(e2e_dir, "test.list"))
+    monkeypatch.setattr(utils, "KINETICS_FRAME_DIR", e2e_dir)
+    monkeypatch.setitem(utils.EPISODE_NUMS, "test", n_ep)
+    sd = synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0)
+    pkl = str(tmp_path / "model.pkl")
+    torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, pkl)
+
+    random.seed(5)
+    tn = network_test.TestNetwork(str(tmp_path / "acc.txt"), "resnet18", "protonet", True)
+    tn.episodes_per_batch = 3  # two batches, ragged last one
+    tn.test_network_baseline(pre_model=pkl)
+    tn.acc_file.close()
+
+    random.seed(5)
+    lines = open(os.path.join(e2e_dir, "test.list")).readlines()
+    index = harness_ref.class_index(lines)
+    plans = [harness_ref.sample_episode_plan(index, 5, 1) for _ in range(n_ep)]
+
+    def load(vi, support):
+        v, n = frames_ref.load_clip_padded(e2e_dir, vi, "test", T=16)
+        return (torch.from_numpy(v), n) if support else (torch.from_numpy(v[:n]), n)
+
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    model = resnet_ref.build_model("resnet18", sd)
+    ref = harness_ref.run_baseline(model, plans, load, L2=True, kind="protonet")
+    assert [int(np.asarray(r["pred"]).reshape(-1)[0]) for r in ref] == [int(p) for p in tn.last_preds]
