@@ -88,6 +88,8 @@ bool conv_bf16_p8_default(const ConvArgs& a);
 int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
+bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv
+int launch_conv_rows_x3(const ConvArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ layout / pooling
 // stem input layout: zero-bordered RGB rows of stem_row_pixels(W, pad) pixels (even, so the

@@ -435,6 +435,11 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  static const int x3rows = [] {
+    const char* e = getenv("EOSV_X3_ROWS");  // 0 = f32x3 stage-1 3x3 convs on the tap-shift kernel (A/B switch)
+    return e ? atoi(e) : 1;
+  }();
+  if (x3rows && conv_rows_x3_ok(a)) return launch_conv_rows_x3(a, s);
   // tap-shift kernel (conv_bf16_ts.hip) for the stride-1 3x3 convs with Cout = 128 (r01g A/B: 5-6 %
   // faster) and the f32x3 Cout = 64 convs (512x64: 10-12 % faster than 256x64); at Cout >= 256
   // its 64-B rows lost 2-8 % to the 256x256 im2col tile

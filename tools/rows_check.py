@@ -1,5 +1,6 @@
-"""A/B correctness for a conv-kernel env switch: dump bf16 backbone features (R18, R50) for a
-few batch sizes in one process, compare two dumps bitwise in another.
+"""A/B correctness for a conv-kernel env switch: dump backbone features (R18, R50; DTYPE env,
+default bf16) for a few batch sizes in one process, compare two dumps in another (bitwise;
+with TOL set, max relative difference <= TOL passes).
 
   EOSV_BF16_ROWS=1 python tools/rows_check.py dump gpurun_out/rows_1.npz
   EOSV_BF16_ROWS=2 python tools/rows_check.py dump gpurun_out/rows_2.npz
@@ -19,7 +20,7 @@ def dump(path):
     out = {}
     for name in ("resnet18", "resnet50"):
         sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
-        bb = engine.Backbone(name, "bf16", 224, 224, max_frames=300)
+        bb = engine.Backbone(name, os.environ.get("DTYPE", "bf16"), 224, 224, max_frames=300)
         bb.load_state_dict(sd)
         for n in (1, 19, 37, 300):
             x = torch.randn(n, 3, 224, 224, generator=torch.Generator().manual_seed(n)).cuda()
@@ -36,7 +37,7 @@ def compare(a, b):
         same = np.array_equal(da[k].view(np.uint32), db[k].view(np.uint32))
         rel = np.abs(da[k] - db[k]).max() / max(np.abs(da[k]).max(), 1e-30)
         print(f"{k}: {'bit-identical' if same else 'DIFFERENT'} max rel {rel:.3g}")
-        bad += not same
+        bad += not same and not (os.environ.get("TOL") and rel <= float(os.environ["TOL"]))
     sys.exit(1 if bad else 0)
 
 
