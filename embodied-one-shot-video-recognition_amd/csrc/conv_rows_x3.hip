@@ -59,7 +59,9 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
 }
 }  // namespace
 
-template <bool RES>
+// ABL (profiling-only instance, EOSV_CONV_ABL bits, results wrong): 1 no prefetch DMA, 2 no residual
+// loads, 16 no ds_reads, 32 no MFMAs, 64 no stores
+template <bool RES, bool ABL>
 __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrips) {
   __shared__ __attribute__((aligned(16))) u16 In[2 * BUF];
 
@@ -138,12 +140,13 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
   int cur = 0;
   for (; strip < nstrips; strip += G) {
     const int next = strip + G;
-    if (next < nstrips) stage(next, cur ^ 1);
+    const int abl = ABL ? a.abl : 0;
+    if (next < nstrips && !(abl & 1)) stage(next, cur ^ 1);
     const int img = strip / spi;
     const int y0 = (strip - img * spi) * TR;
     const long long obase = ((long long)img * H + y0) * RW * PIX;
-    uint2 rh[TILES], rl[TILES];
-    if constexpr (RES) {
+    uint2 rh[TILES] = {}, rl[TILES] = {};
+    if (RES && (!ABL || (res && !(abl & 2)))) {  // the ABL instance runs every layer, res or not
 #pragma unroll
       for (int i = 0; i < TILES; ++i) {
         const u16* src = res + obase + (long long)(i * 16 + r16) * PIX + 16 * g + 4 * q;
@@ -162,10 +165,11 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
     f32x4 acc[TILES];
 #pragma unroll
     for (int i = 0; i < TILES; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 xh[2][TILES], xl[2][TILES];
+    bf16x8 xh[2][TILES] = {}, xl[2][TILES] = {};
     // one add + the hi and lo reads per tile in one asm, so hipcc cannot hoist the 126
     // summed addresses out of the unrolled k-loop
     auto frags = [&](int t, int b) {
+      if (abl & 16) return;
 #pragma unroll
       for (int i = 0; i < TILES; ++i) {
         unsigned tmp;
@@ -185,12 +189,14 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
       if (t + 1 < 18) frags(t + 1, (t + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
       const int b = t & 1;
+      if (!(abl & 32)) {
 #pragma unroll
-      for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[t], xh[b][i], acc[i], 0, 0, 0);
+        for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[t], xh[b][i], acc[i], 0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[t], xh[b][i], acc[i], 0, 0, 0);
+        for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[t], xh[b][i], acc[i], 0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[t], xl[b][i], acc[i], 0, 0, 0);
+        for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[t], xl[b][i], acc[i], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -221,12 +227,14 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
       const uint2 hv = make_uint2((unsigned)hb[0] | ((unsigned)hb[1] << 16), (unsigned)hb[2] | ((unsigned)hb[3] << 16));
       const uint2 lv = make_uint2((unsigned)lb[0] | ((unsigned)lb[1] << 16), (unsigned)lb[2] | ((unsigned)lb[3] << 16));
       u16* dst = y + obase + (long long)(i * 16 + r16) * PIX + 16 * g + 4 * q;
+      if (abl & 64) continue;
       asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(hv) : "memory");
       asm volatile("global_store_dwordx2 %0, %1, off offset:128" ::"v"(dst), "v"(lv) : "memory");
       asm volatile("global_store_dwordx2 %0, %1, off offset:256" ::"v"(dst), "v"(hv) : "memory");
     }
     // the next strip's DMA (issued before this strip's 21 stores) has landed, and every wave's
     // reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
+    if (abl & 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
@@ -252,10 +260,12 @@ int launch_conv_rows_x3(const ConvArgs& a, hipStream_t s) {
   if (nstrips <= 0) return EOSV_OK;
   if (nstrips > 0x7fffffffLL) return set_error("conv_rows_x3: too many strips"), EOSV_ERR_UNSUPPORTED;
   const unsigned grid = (unsigned)std::min<long long>(nstrips, ncu);
-  if (a.res)
-    hipLaunchKernelGGL(conv_rows_x3_kernel<true>, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
+  if (a.abl)
+    hipLaunchKernelGGL((conv_rows_x3_kernel<true, true>), dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
+  else if (a.res)
+    hipLaunchKernelGGL((conv_rows_x3_kernel<true, false>), dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
   else
-    hipLaunchKernelGGL(conv_rows_x3_kernel<false>, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
+    hipLaunchKernelGGL((conv_rows_x3_kernel<false, false>), dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
