@@ -141,3 +141,47 @@ def test_episode_sharding_gloo(world, tmp_path):
     plans = episodes.sample_episodes(37, 5, 1, "test", seed=11)
     assert res["accs"] == [float(p["query_y"] == e) for p, e in zip(plans, expect)]
     assert res["t"] == float(world) and res["n"] == 37
+
+
+def test_jpeg_clip_window_draws_follow_reference_order(tmp_path):
+    """JpegFrames (GPU ingest path) host logic: decode + narrow-frame resize, and the train-mode
+    window/flip drawn from `random` then `torch` exactly as the restated reference loader
+    (oracle/frames_ref.py, utils.py:57-78) draws them -- checked without a GPU."""
+    from PIL import Image
+
+    from eosv import frames as fr
+
+    d = tmp_path / "c" / "v"
+    d.mkdir(parents=True)
+    rng = np.random.default_rng(1)
+    for f in (1, 2):
+        Image.fromarray(rng.integers(0, 256, size=(150, 200, 3), dtype=np.uint8)).save(d / ("image_%05d.jpg" % f))
+    src = fr.JpegFrames(str(tmp_path), crop=224, init_h=256)
+    a = src.decode(str(d / "image_00001.jpg"))
+    assert a.shape == (256, 224, 3) and a.dtype == np.uint8  # resized like utils.py:123-124
+    for seed in range(5):
+        random.seed(seed)
+        torch.manual_seed(seed)
+        got = src.window(a, "train")
+        random.seed(seed)
+        torch.manual_seed(seed)
+        flip = random.random() < 0.5
+        ij = (int(torch.randint(0, 256 - 224 + 1, size=(1,)).item()), int(torch.randint(0, 1, size=(1,)).item()))
+        assert got == (ij, flip)
+    assert src.window(a, "test") == (None, False)
+    sq = np.zeros((224, 224, 3), np.uint8)
+    torch.manual_seed(0)
+    before = torch.get_rng_state()
+    assert src.window(sq, "train")[0] == (0, 0)
+    assert torch.equal(before, torch.get_rng_state())  # crop-sized frame: torchvision draws nothing
+
+
+def test_crop_normalize_rejects_bad_window():
+    """eosv_crop_normalize_frames validates its window before touching the device."""
+    L = _lib.lib()
+    m = (ctypes.c_float * 3)(0.5, 0.5, 0.5)
+    assert L.eosv_crop_normalize_frames(None, 0, 240, 320, 224, 0, 0, 0, m, m, None, None) == 0  # empty
+    assert L.eosv_crop_normalize_frames(None, 1, 240, 320, 224, 17, 0, 0, m, m, None, None) == -1  # past H
+    assert L.eosv_crop_normalize_frames(None, 1, 240, 320, 224, 0, -1, 0, m, m, None, None) == -1
+    assert b"window" in L.eosv_last_error()
+    assert L.eosv_normalize_frames(None, 1, 200, 320, 224, m, m, None, None) == -1  # H < crop
