@@ -13,13 +13,14 @@
 //    to stem conv -> shift -> ReLU -> maxpool on the same accumulators.
 //
 // MFMA: v_mfma_f32_16x16x4_f32 (exact f32, a k-ordered fma chain) with D = W . X^T (rows =
-// output channels, columns = stem pixels), K = [kh 7][24] (kw*3 + c, 21 real + 3 zero weights
-// per kernel row) = 168 = 42 k-steps of 4; the 4 k of a step share one kernel row (24 = 6 x 4),
-// so step s reads input row 2*sy + s/6, elements 6*sx + 4*(s%6) + q: one ds_read_b32 per lane.
-// Weights live in LDS permuted so that one ds_read_b128 gives a lane its A values for 4
-// consecutive steps: Wl[j][t][r16][q][i] = W[16j + r16][16t + 4i + q].
+// output channels, columns = stem pixels), dense K = [kh 7][21] (kw*3 + c) + 1 zero = 148 = 37
+// k-steps of 4 (the padded [kh][24] layout took 42).  Element k of lane q's step reads input
+// row 2*sy + k/21, element 6*sx + k%21: a step whose 4 k straddle two kernel rows picks the
+// row base per lane (one v_cndmask between two wave-uniform bases), so it is still one
+// ds_read_b32 per lane.  Weights live in LDS permuted so that one ds_read_b128 gives a lane
+// its A values for 4 consecutive steps: Wl[j][t][r16][q][i] = W[16j + r16][16t + 4i + q].
 //
-// LDS: weights 44 KiB | a ring of 13 input rows (row r in slot r % 13; a step needs rows
+// LDS: weights 40 KiB | a ring of 13 input rows (row r in slot r % 13; a step needs rows
 // 4py .. 4py+8 and prefetches 4py+9 .. 4py+12), each row Wp * 3 floats padded to 16 B,
 // filled by LDS-DMA from the dense padded RGB pack (8-B aligned sources).  ~80 KiB: two
 // workgroups (16 waves) per CU.
@@ -33,11 +34,12 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int SPF_MAX_TILES = 8;   // pooled width <= 56
-constexpr int SPF_STEPS = 42;      // k-steps of 4 over K = 168
-constexpr int SPF_GROUPS = 11;     // b128 weight groups of 4 steps (44 steps, the last 2 zero)
+constexpr int SPF_K = 147;         // real K: 7 kernel rows x 21 (kw*3 + c)
+constexpr int SPF_STEPS = 37;      // k-steps of 4 over dense K = 148
+constexpr int SPF_GROUPS = 10;     // b128 weight groups of 4 steps (40 steps, the last 3 zero)
 constexpr int SPF_KW = 176;        // uploaded f32 stem weight row ([kh][24] + 8 zero)
 constexpr int SPF_RING = 13;
-constexpr int SPF_W_FLOATS = 4 * SPF_GROUPS * 16 * 16;  // 11264 floats = 44 KiB
+constexpr int SPF_W_FLOATS = 4 * SPF_GROUPS * 16 * 16;  // 10240 floats = 40 KiB
 
 __host__ __device__ constexpr int spf_row_floats(int Wp) { return (Wp * 3 + 3) & ~3; }
 
@@ -81,8 +83,8 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
   // weights -> LDS, permuted (see header); plain loads, once per image
   for (int e = tid; e < SPF_W_FLOATS; e += blockDim.x) {
     const int i = e & 3, qq = (e >> 2) & 3, rr = (e >> 4) & 15, t = (e >> 8) % SPF_GROUPS, j = e / (256 * SPF_GROUPS);
-    const int k = 16 * t + 4 * i + qq;
-    Wl[e] = k < SPF_KW ? w[(j * 16 + rr) * SPF_KW + k] : 0.f;
+    const int k = 16 * t + 4 * i + qq;  // dense k -> uploaded [kh][24] column
+    Wl[e] = k < SPF_K ? w[(j * 16 + rr) * SPF_KW + 24 * (k / 21) + k % 21] : 0.f;
   }
   f32x4 bv[4];
 #pragma unroll
@@ -104,11 +106,14 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
   // this lane's stem column; columns outside the map enter the pool as -inf (clamped read)
   const int sx = 14 * wid - 1 + r16;
   const bool colok = sx >= 0 && sx < Ws;
-  const int xoff = 6 * max(sx, 0) + q;  // + 4 * (s % 6) per step
+  const int xoff = 6 * max(sx, 0) + q;  // + ring row base + 4s - 21 kh per step
 
   auto stem_row = [&](int sy, f32x4 (&acc)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int rowb[7];  // ring offsets of input rows 2sy .. 2sy + 6 (wave-uniform)
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) rowb[kh] = ((2 * sy + kh) % SPF_RING) * RF;
 #pragma unroll
     for (int t = 0; t < SPF_GROUPS; ++t) {
       f32x4 wa[4];
@@ -118,8 +123,14 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
       for (int i = 0; i < 4; ++i) {
         const int s = 4 * t + i;
         if (s >= SPF_STEPS) break;
-        const int kh = s / 6;
-        const float xb = ring[((2 * sy + kh) % SPF_RING) * RF + xoff + 4 * (s - 6 * kh)];
+        // k = 4s + q lies in kernel row kh0 for q < qs, else kh0 + 1 (the zero-weight k = 147
+        // stays in row 6 and reads a real element)
+        const int kh0 = (4 * s) / 21;
+        const int qs = kh0 < 6 ? 21 * (kh0 + 1) - 4 * s : 4;
+        const int b0 = rowb[kh0] + 4 * s - 21 * kh0;
+        int off = b0;
+        if (qs < 4) off = q < qs ? b0 : rowb[kh0 + 1] + 4 * s - 21 * (kh0 + 1);
+        const float xb = ring[off + (kh0 == 6 && s == SPF_STEPS - 1 && q == 3 ? xoff - 1 : xoff)];
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[j][i], xb, acc[j], 0, 0, 0);
       }
