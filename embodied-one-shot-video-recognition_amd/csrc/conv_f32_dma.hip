@@ -329,8 +329,9 @@ int launch_conv_f32_dma(const ConvArgs& a0, hipStream_t s, int variant) {
     if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
     return launch_dma<128, 128, 16, 2, 2, false>(a, s);
   }
-  if (variant == 11) {  // per-layer best of 5/9 (r01 A/B: 256x128 wins 2-3% at Cout 128/256, loses at 512)
-    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
+  if (variant == 11) {  // per-layer best of 5/9 (r01 A/B: 256x128 wins 2-3% at Cout 128/256, loses at 512;
+                        // r01l: 256x64 of 4 waves of 64x64 wins 0.3-2% at Cout 64)
+    if (a.Cout <= 64) return launch_dma<256, 64, 16, 4, 1, false>(a, s);
     if (a.Cout <= 256) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
     return launch_dma<128, 128, 16, 2, 2, false>(a, s);
   }
