@@ -207,7 +207,7 @@ def main():
     T = args.segments * args.seg_len
     E = args.episodes_per_step
     n_steps = args.warmup + args.steps
-    plans = ep_mod.sample_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed)
+    plans = ep_mod.plan_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed)
     mine_idx = edist.shard_indices(len(plans), rank, world)  # episode e runs on rank e % world
     batches = []
     for s in range(n_steps):

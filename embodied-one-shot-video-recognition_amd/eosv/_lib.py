@@ -22,7 +22,7 @@ _STATUS = {-1: "EOSV_ERR_ARG", -2: "EOSV_ERR_HIP", -3: "EOSV_ERR_OOM",
 # every symbol include/eosv.h declares
 EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_fc_forward",
            "eosv_clip_embed", "eosv_segment_mean", "eosv_match", "eosv_segment_match", "eosv_segment_match_episodes",
-           "eosv_temporal_smooth", "eosv_normalize_frames", "eosv_crop_normalize_frames", "eosv_synth_frames", "eosv_profile_enable", "eosv_profile_read", "eosv_feature_dim", "eosv_device_bytes", "eosv_last_error",
+           "eosv_temporal_smooth", "eosv_normalize_frames", "eosv_crop_normalize_frames", "eosv_synth_frames", "eosv_plan_episodes", "eosv_profile_enable", "eosv_profile_read", "eosv_feature_dim", "eosv_device_bytes", "eosv_last_error",
            "eosv_destroy")
 
 
@@ -63,6 +63,7 @@ def lib():
         "eosv_normalize_frames": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp]),
         "eosv_crop_normalize_frames": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
         "eosv_synth_frames": (i32, [vp, i32, i32, i32, vp, vp]),
+        "eosv_plan_episodes": (i32, [vp, i32, i32, i32, ctypes.c_uint64, i32, vp, vp, vp]),
         "eosv_profile_enable": (i32, [vp, i32]),
         "eosv_profile_read": (i32, [vp, vp, vp, vp, i32]),
         "eosv_feature_dim": (i32, [vp]),

@@ -59,6 +59,41 @@ def sample_episodes(n: int, n_way: int = 5, k_shot: int = 1, mode: str = "test",
     return [sample_episode(index, n_way, k_shot, rnd) for _ in range(n)]
 
 
+def plan_episodes(n: int, n_way: int = 5, k_shot: int = 1, mode: str = "test", seed: int = 0,
+                  lines=None) -> List[dict]:
+    """The native plan service (csrc/plan.hip ``eosv_plan_episodes``): the same plans as
+    ``sample_episodes(n, n_way, k_shot, mode, seed=seed)``, drawn in C++ from a restated
+    CPython MT19937 without a per-episode dict rebuild.  ``seed``: int in [0, 2**64)."""
+    import ctypes
+
+    import numpy as np
+
+    from . import _lib
+
+    index = class_index(lines if lines is not None else read_list(mode))
+    names = list(index.keys())
+    sizes = np.array([len(index[c]) for c in names], dtype=np.int32)
+    classes = np.zeros((max(n, 1), n_way), dtype=np.int32)
+    query = np.zeros((max(n, 1), 2), dtype=np.int32)
+    support = np.zeros((max(n, 1), n_way, max(k_shot, 1)), dtype=np.int32)
+    if not 0 <= int(seed) < 2 ** 64:
+        raise ValueError("plan_episodes: seed must be in [0, 2**64)")
+    _lib.check(_lib.lib().eosv_plan_episodes(sizes.ctypes.data, len(names), n_way, k_shot, ctypes.c_uint64(int(seed)),
+                                             n, classes.ctypes.data, query.ctypes.data, support.ctypes.data),
+               "eosv_plan_episodes")
+    plans = []
+    for e in range(n):
+        cls = [names[c] for c in classes[e]]
+        qpos = int(query[e, 0])
+        sup, sup_y = [], []
+        for i, c in enumerate(cls):
+            for s in range(k_shot):
+                sup.append(index[c][support[e, i, s]])
+                sup_y.append(i)
+        plans.append(dict(support=sup, support_y=sup_y, query=index[cls[qpos]][query[e, 1]], query_y=qpos))
+    return plans
+
+
 def shard(episodes: Sequence[dict], rank: int, world: int) -> List[dict]:
     """Episodes e with e % world == rank."""
     return [ep for i, ep in enumerate(episodes) if i % world == rank]

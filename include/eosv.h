@@ -152,6 +152,18 @@ int eosv_synth_frames(const uint64_t* d_params, int n_frames, int H, int W, floa
 int eosv_profile_enable(eosv_handle* h, int enable);
 int eosv_profile_read(eosv_handle* h, double* ms, double* flops, int64_t* launches, int max_layers);
 
+/* Episode-plan service (host only, no device call): n_episodes n-way k-shot plans in the
+ * reference's RNG order (episode_novel_dataloader.py:35-70 drawing from Python's `random`
+ * seeded with random.seed(seed)); replaces the per-episode dict rebuild + random.sample calls
+ * of EpisodeDataloader.get_episode (episode_novel_dataloader.py:19-80).
+ * class_sizes[c] = number of videos of class c, classes in the split list's first-appearance
+ * order.  Outputs: classes [E][n_way] (class ids in sampled order; support label = position),
+ * query [E][2] (position of the query class, video index in that class), support
+ * [E][n_way][k_shot] (video indices, class by class).  EOSV_ERR_ARG where random.sample would
+ * raise (a class with fewer videos than drawn, n_way > n_classes). */
+int eosv_plan_episodes(const int32_t* class_sizes, int n_classes, int n_way, int k_shot, uint64_t seed,
+                       int n_episodes, int32_t* classes, int32_t* query, int32_t* support);
+
 /* Feature dimension D of the handle's backbone. */
 int eosv_feature_dim(const eosv_handle* h);
 

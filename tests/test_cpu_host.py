@@ -53,6 +53,36 @@ def test_product_episode_sampler_matches_reference_plans():
         assert a == {k: b[k] for k in ("support", "support_y", "query", "query_y")}
 
 
+def test_native_plan_service_matches_reference_plans():
+    """csrc/plan.hip (host-only C-ABI call) against the plans captured from the reference."""
+    meta, _ = load_fixture("plans_test_seed0")
+    got = episodes.plan_episodes(len(meta["episodes"]), 5, 1, "test", seed=meta["seed"])
+    for a, b in zip(got, meta["episodes"]):
+        assert a == {k: b[k] for k in ("support", "support_y", "query", "query_y")}
+
+
+# both Random.sample strategies: 24 test classes / ~100 videos per class take the rejection
+# set (k <= 5 -> setsize 21); n_way 20 (setsize 85) and the 14 x 10 synthetic list take the pool
+@pytest.mark.parametrize("n,n_way,k_shot,seed,small", [(300, 5, 5, 7, False), (200, 3, 2, 2 ** 40 + 5, False),
+                                                       (100, 20, 1, 123, False), (50, 5, 0, 9, False),
+                                                       (200, 14, 1, 4, True), (100, 5, 8, 0, True)])
+def test_native_plan_service_matches_python_sampler(n, n_way, k_shot, seed, small):
+    lines = [f"c{c:02d}/v{v}\n" for c in range(14) for v in range(10)] if small else None
+    want = episodes.sample_episodes(n, n_way, k_shot, "test", seed=seed, lines=lines)
+    assert episodes.plan_episodes(n, n_way, k_shot, "test", seed=seed, lines=lines) == want
+
+
+def test_native_plan_service_errors_like_random_sample():
+    lines = [f"c{c}/v{v}\n" for c in range(6) for v in range(3)]
+    with pytest.raises(_lib.EosvError, match="Sample larger"):
+        episodes.plan_episodes(4, 7, 1, "test", seed=0, lines=lines)   # n_way > classes
+    with pytest.raises(_lib.EosvError, match="Sample larger"):
+        episodes.plan_episodes(4, 5, 3, "test", seed=0, lines=lines)   # query class needs k + 1 = 4 > 3
+    with pytest.raises(ValueError):
+        random.Random(0).sample(range(3), 4)
+    assert episodes.plan_episodes(0, 5, 1, "test", seed=0) == []
+
+
 def test_dropin_dataloader_matches_reference_episodes():
     import episode_novel_dataloader
     import utils
