@@ -105,6 +105,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
     brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 4 : nullptr;
   }
 
+  // tap of the next A stage, advanced per stage call (k0 grows by BK; Cin % BK == 0): no
+  // per-K-step divisions by Cin and KW
+  int nc0 = 0, nkw = 0, nkh = 0;
   auto stage = [&](int k0, int slot) {
     float* As = smem + slot * STAGE;
     float* Bs = As + BM * BK;
@@ -126,11 +129,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     } else {
-      const int tap = k0 / a.Cin;
-      const int c0 = k0 - tap * a.Cin;
-      const int kh = tap / a.KW;
-      const int kw = tap - kh * a.KW;
-      const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;  // wave-uniform
+      const int kh = nkh, kw = nkw;
+      const long long toff = ((long long)kh * a.W + kw) * a.Cin + nc0;  // wave-uniform
+      nc0 += BK;
+      if (nc0 == a.Cin) {
+        nc0 = 0;
+        if (++nkw == a.KW) nkw = 0, ++nkh;
+      }
 #pragma unroll
       for (int j = 0; j < AI; ++j) {
         const int ih = aih[j] + kh, iw = aiw[j] + kw;
