@@ -12,6 +12,17 @@ namespace eosv {
 
 void set_error(const std::string& msg);
 
+// A/B switches and profiling ablations exist only in the profiling build (`make prof` ->
+// libeosv_prof.so, -DEOSV_PROFILING; tools/ select it with EOSV_LIBRARY).  In the release
+// library every switch is its compile-time default and no environment variable is read.
+#ifdef EOSV_PROFILING
+int env_switch(const char* name, int dflt);
+#define EOSV_ABL(a) ((a).abl)
+#else
+constexpr int env_switch(const char*, int dflt) { return dflt; }
+#define EOSV_ABL(a) 0
+#endif
+
 #define EOSV_HIP_CHECK(expr)                                                               \
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \
@@ -45,8 +56,6 @@ struct ConvArgs {
   const void* zero;   // >= 64 zeroed bytes (DMA target for out-of-bounds taps)
   int abl;            // ablation bits for profiling builds (0 = normal)
   int xcd;            // 1: XCD-aware block order (each XCD walks a contiguous range of tiles)
-  int p8pipe;         // conv_bf16_p8: 1 counted-vmcnt half-tile pipeline, 0 former vmcnt(0) per K-tile
-  int p8prio;         // conv_bf16_p8: 1 s_setprio(1) around the MFMA segments
   int kcm;            // bf16 only: K ordered (cin/64, kh, kw, cin%64) instead of (kh, kw, cin)
   // fused 1x1 downsample (ResNet block shortcut): K columns [K1, K) read x2 at output pixel
   // (oh, ow) -> x2 pixel (oh * stride2, ow * stride2), channel k - K1; nullptr = none
@@ -70,7 +79,6 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int on) {
 }
 
 int launch_conv_f32(const ConvArgs& a, hipStream_t s);
-int launch_conv_f32_dma(const ConvArgs& a, hipStream_t s, int variant);
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 bool conv_bf16_ts_ok(const ConvArgs& a);  // conv_bf16_ts.hip: tap-shift stride-1 3x3 convs
 int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s);
@@ -83,9 +91,6 @@ int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w,
 bool stem_pool_f32_ok(int H, int W);  // stem_pool_f32.hip: the same for f32
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                          hipStream_t s, bool split = false);  // split: y in the EOSV_F32X3 (hi, lo, hi) layout
-bool conv_bf16_p8_ok(const ConvArgs& a);  // conv_bf16_p8.hip: phased 8-wave implicit GEMM
-bool conv_bf16_p8_default(const ConvArgs& a);
-int launch_conv_bf16_p8(const ConvArgs& a, hipStream_t s);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv

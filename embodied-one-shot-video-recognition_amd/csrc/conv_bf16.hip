@@ -52,7 +52,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int M = a.N * HoWo;
   const int nN = (a.Cout + BN - 1) / BN;
   const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
-  if (a.abl & 512) return;  // profiling-only: dispatch cost alone
+  if (EOSV_ABL(a) & 512) return;  // profiling-only: dispatch cost alone
   const int mt = bt / nN;
   const int nt = bt - mt * nN;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const int r = lane & (MF - 1);
   const int q = lane / MF;
   const int sw = (r >> 1) & 7;  // tile bases are multiples of 16 rows: the swizzle depends on r only
-  const int nk = (a.abl & 1024) ? 0 : a.K / BK;  // 1024 (profiling-only): no K-loop
+  const int nk = (EOSV_ABL(a) & 1024) ? 0 : a.K / BK;  // 1024 (profiling-only): no K-loop
   // NS-deep ring: NS-1 stages in flight; with NS = 3 the wait before each barrier is a
   // counted vmcnt (the newest stage stays in flight across it) and barriers are raw
   // s_barrier (__syncthreads would drain it with vmcnt(0))
@@ -185,9 +185,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   int cur = 0, wslot = NS - 1;
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
-    // a.abl (profiling-only ablations, results wrong when set): 1 no main-loop loads,
+    // EOSV_ABL(a) (profiling-only ablations, results wrong when set): 1 no main-loop loads,
     // 4 no A loads, 8 no B loads, 16 no ds_reads, 32 no MFMAs, 64 no epilogue
-    if (issue && !(a.abl & 1)) stage((kt + NS - 1) * BK, wslot, a.abl);
+    if (issue && !(EOSV_ABL(a) & 1)) stage((kt + NS - 1) * BK, wslot, EOSV_ABL(a));
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
     constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     for (int s = 0; s < BK / KS; ++s) {
       const int pch = ((s * (KS / 8) + q) ^ sw) * 8;
       bf16x8 af[TM], bf[TN];
-      if (a.abl & 16) {  // profiling-only: no ds_reads (operands stay whatever the registers hold)
+      if (EOSV_ABL(a) & 16) {  // profiling-only: no ds_reads (operands stay whatever the registers hold)
 #pragma unroll
         for (int i = 0; i < TM; ++i) af[i] = bf16x8{};
 #pragma unroll
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) bf[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * MF + r) * BK + pch);
       }
-      if (a.abl & 32) {  // profiling-only: no MFMAs
+      if (EOSV_ABL(a) & 32) {  // profiling-only: no MFMAs
         asm volatile("" ::"v"(af[0]), "v"(bf[0]));
         continue;
       }
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     wslot = wslot + 1 == NS ? 0 : wslot + 1;
   }
 
-  if (a.abl & 64) {  // profiling-only: no epilogue
+  if (EOSV_ABL(a) & 64) {  // profiling-only: no epilogue
     asm volatile("" ::"v"(acc[0][0][0]));
     return;
   }
@@ -359,19 +359,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   }
 }
 
-static int bf16_mfma() {
-  static int v = [] {
-    const char* e = getenv("EOSV_BF16_MFMA");  // 32 or 16 (A/B switch)
-    return e ? atoi(e) : 16;
-  }();
-  return v;
-}
-
 static int bf16_rows() {
-  static int v = [] {
-    const char* e = getenv("EOSV_BF16_ROWS");  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
-    return e ? atoi(e) : 1;
-  }();
+  static int v = env_switch("EOSV_BF16_ROWS", 1);  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
   return v;
 }
 
@@ -393,9 +382,6 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
     if (STEM || a.K1 % 64 || a.Cin2 % 64) return set_error("conv_bf16: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
     hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
                        s, a);
-  } else if (bf16_mfma() == 32) {
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 32, NS, false>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
-                       s, a);
   } else {
     hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS, false>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
                        s, a);
@@ -404,27 +390,8 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   return EOSV_OK;
 }
 
-static int bf16_p8() {
-  static int v = [] {
-    const char* e = getenv("EOSV_BF16_P8");  // 0 never, 1 default shapes, 2 every eligible shape (A/B switch)
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-static int bf16_variant() {
-  static int v = [] {
-    const char* e = getenv("EOSV_BF16_TILE");
-    return e ? atoi(e) : 3;
-  }();
-  return v;
-}
-
 int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
-  static const int abl = [] {
-    const char* e = getenv("EOSV_CONV_ABL");  // profiling-only ablations; results are wrong when set
-    return e ? atoi(e) : 0;
-  }();
+  static const int abl = env_switch("EOSV_CONV_ABL", 0);  // profiling-only ablations; results are wrong when set
   ConvArgs a = a0;
   a.abl = abl;
   const bool stem = (a.Cin == 3);
@@ -435,43 +402,26 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
-  static const int x3rows = [] {
-    const char* e = getenv("EOSV_X3_ROWS");  // 0 = f32x3 stage-1 3x3 convs on the tap-shift kernel (A/B switch)
-    return e ? atoi(e) : 1;
-  }();
+  static const int x3rows = env_switch("EOSV_X3_ROWS", 1);  // 0 = f32x3 stage-1 3x3 convs on the tap-shift kernel (A/B switch)
   if (x3rows && conv_rows_x3_ok(a)) return launch_conv_rows_x3(a, s);
   // tap-shift kernel (conv_bf16_ts.hip) for the stride-1 3x3 convs with Cout = 128 (r01g A/B: 5-6 %
   // faster) and the f32x3 Cout = 64 convs (512x64: 10-12 % faster than 256x64); at Cout >= 256
   // its 64-B rows lost 2-8 % to the 256x256 im2col tile
-  static const int ts = [] {
-    const char* e = getenv("EOSV_BF16_TS");  // 0 never, 1 default shapes, 2 every eligible shape (A/B switch)
-    return e ? atoi(e) : 1;
-  }();
+  static const int ts = env_switch("EOSV_BF16_TS", 1);  // 0 never, 1 default shapes, 2 every eligible shape (A/B switch)
   if (ts && conv_bf16_ts_ok(a) && (ts == 2 || a.Cout == 128 || (a.Cout == 64 && a.split)))
     return launch_conv_bf16_ts(a, s);
-  if (bf16_p8() && conv_bf16_p8_ok(a) && (bf16_p8() == 2 || conv_bf16_p8_default(a))) return launch_conv_bf16_p8(a, s);
   // r01 A/B: 256x128 tiles for Cout 128 and 128x128 / 128x256 tiles for the
-  // K = 64 1x1 convs all measured slower than this choice
-  const int v = bf16_variant();
-  // f32x3 (K tripled): 256x64 tiles for the Cout-64 stage-1 convs, +7 % over 128x64 (r01 A/B,
-  // tools/ab_x3.sh)
-  if (a.split && a.Cout <= 64 && v == 3) return launch_bf16<256, 64, 4, 1, false>(a, s);
+  // K = 64 1x1 convs all measured slower than this choice.
+  // f32x3 (K tripled): 256x64 tiles for the Cout-64 convs, +7 % over 128x64 (tools/ab_x3.sh)
+  if (a.split && a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);
   // Cout 128 (ResNet stage 2, R50 bottleneck 1x1s, stride-2 entries and the fused downsample):
   // 512x128 tiles (160 KiB, 8 waves of 128x64), the one-barrier-per-K-step loop of the 256x256
-  // tile.  r01 A/B (tools/ab_sets.sh): 12-15 % faster than the phased conv_bf16_p8 512x128 (whose 8
+  // tile.  r01 A/B (tools/ab_sets.sh): 12-15 % faster than a phased 8-wave 512x128 kernel (whose 8
   // barriers per K-tile cost more than its overlap gains: SQ MFMA-busy 0.29 vs 0.42) and 5 %
   // faster than 128x128 on the stride-2 entry.
-  if ((v == 3 || v == 10) && a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
-  if (v == 8 && a.Cout == 128) return launch_bf16<256, 128, 4, 2, false, 3>(a, s);  // 144 KiB, 1 block/CU
-  if (v == 9 && a.Cout == 128) return launch_bf16<128, 128, 2, 2, false, 3>(a, s);  // 96 KiB
-  if ((v == 3 || v == 8 || v == 9) && a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
-  if (bf16_variant() == 2) {  // 256x256 tiles, 8 waves of 128x64
-    if (a.Cout <= 64) return launch_bf16<256, 64, 4, 1, false>(a, s);
-    if (a.Cout <= 128) return launch_bf16<256, 128, 4, 2, false>(a, s);
-    return launch_bf16<256, 256, 2, 4, false>(a, s);
-  }
-  if (a.Cout <= 64) return launch_bf16<128, 64, 2, 2, false>(a, s);
-  return launch_bf16<128, 128, 2, 2, false>(a, s);
+  if (a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
+  if (a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
+  return launch_bf16<128, 64, 2, 2, false>(a, s);
 }
 
 }  // namespace eosv

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   int slot = 0, wslot = NS - 1;
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
-    if (issue && !(a.abl & 1)) stage((kt + NS - 1) * BK, wslot);
+    if (issue && !(EOSV_ABL(a) & 1)) stage((kt + NS - 1) * BK, wslot);
     const float* As = smem + slot * STAGE;
     const float* Bs = As + BM * BK;
 #pragma unroll
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
             v.z = fmaxf(v.z, 0.f);
             v.w = fmaxf(v.w, 0.f);
           }
-          if (a.abl & 2)
+          if (EOSV_ABL(a) & 2)
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
           else
             *(float4*)(y + o) = v;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
           float v = acc[i][j][q] + bcol[j];
           if (res) v += res[o];
           if (a.relu) v = fmaxf(v, 0.f);
-          if (a.abl & 2) asm volatile("" ::"v"(v)); else y[o] = v;
+          if (EOSV_ABL(a) & 2) asm volatile("" ::"v"(v)); else y[o] = v;
         }
       }
     }
@@ -303,45 +303,27 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
   return EOSV_OK;
 }
 
-// variant 2: BK 32, 128x128 / 128x64 (2 blocks/CU); variant 5: BK 16 (4 blocks/CU)
-int launch_conv_f32_dma(const ConvArgs& a0, hipStream_t s, int variant) {
-  static const int abl = [] {
-    const char* e = getenv("EOSV_CONV_ABL");  // profiling-only ablations; results are wrong when set
-    return e ? atoi(e) : 0;
-  }();
+// Tile per layer (r01 / r01l A/B): 256x64 (4 waves of 64x64) for Cout 64, 256x128
+// (8 waves) for Cout 128 / 256, 128x128 for Cout >= 512, all BK 16 with a 2-deep ring.  The fc
+// head (M = frames, Cout = num_classes) runs here too: when Cout % 4 != 0 its rows are not 16-B
+// aligned, so it takes the per-element epilogue instead of the LDS-staged float4 one.
+int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
-  a.abl = abl;
+  a.abl = env_switch("EOSV_CONV_ABL", 0);  // profiling build only: ablations, results are wrong when set
   const bool stem = (a.Cin == 3);
+  if (!a.zero || (stem && (a.KWp != 8 || a.KW != 7 || a.K != (a.KH * 24 + 15) / 16 * 16)) ||
+      (!stem && (a.K % 32 != 0 || a.Cin % 32 != 0))) {
+    set_error("conv_f32: unsupported shape (K % 32, Cin % 32 or stem layout)");
+    return EOSV_ERR_UNSUPPORTED;
+  }
   if (stem) return launch_dma<128, 64, 16, 2, 2, true>(a, s);
-  if (variant == 6) {  // BK 16, 2-deep ring, per-lane epilogue stores (pre-LDS-epilogue baseline)
-    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);
-    return launch_dma<128, 128, 16, 2, 2, false, 2, false>(a, s);
+  if (a.Cout % 4) {
+    if (a.x2) return set_error("conv_f32: fused downsample needs Cout % 4 == 0"), EOSV_ERR_UNSUPPORTED;
+    return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);
   }
-  if (variant == 7) {  // BK 32, 3-deep ring
-    if (a.Cout <= 64) return launch_dma<128, 64, 32, 2, 2, false, 3>(a, s);
-    return launch_dma<128, 128, 32, 2, 2, false, 3>(a, s);
-  }
-  if (variant == 9) {  // BK 16, 256-row tiles (8 waves for Cout >= 128)
-    if (a.Cout <= 64) return launch_dma<256, 64, 16, 4, 1, false>(a, s);
-    return launch_dma<256, 128, 16, 4, 2, false>(a, s);
-  }
-  if (variant == 10) {  // BK 16, 128x256 for Cout >= 256 (wave 64x128)
-    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
-    if (a.Cout <= 128) return launch_dma<128, 128, 16, 2, 2, false>(a, s);
-    return launch_dma<128, 256, 16, 2, 2, false>(a, s);
-  }
-  if (variant == 5) {
-    if (a.Cout <= 64) return launch_dma<128, 64, 16, 2, 2, false>(a, s);
-    return launch_dma<128, 128, 16, 2, 2, false>(a, s);
-  }
-  if (variant == 11) {  // per-layer best of 5/9 (r01 A/B: 256x128 wins 2-3% at Cout 128/256, loses at 512;
-                        // r01l: 256x64 of 4 waves of 64x64 wins 0.3-2% at Cout 64)
-    if (a.Cout <= 64) return launch_dma<256, 64, 16, 4, 1, false>(a, s);
-    if (a.Cout <= 256) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
-    return launch_dma<128, 128, 16, 2, 2, false>(a, s);
-  }
-  if (a.Cout <= 64) return launch_dma<128, 64, 32, 2, 2, false>(a, s);
-  return launch_dma<128, 128, 32, 2, 2, false>(a, s);
+  if (a.Cout <= 64) return launch_dma<256, 64, 16, 4, 1, false>(a, s);
+  if (a.Cout <= 256) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
+  return launch_dma<128, 128, 16, 2, 2, false>(a, s);
 }
 
 }  // namespace eosv

@@ -261,9 +261,11 @@ int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s) {
   if (nstrips <= 0) return EOSV_OK;
   if (nstrips > 0x7fffffffLL) return set_error("conv_rows: too many strips"), EOSV_ERR_UNSUPPORTED;
   const unsigned grid = (unsigned)std::min<long long>(nstrips, ncu);
+#ifdef EOSV_PROFILING
   if (a.abl)
     hipLaunchKernelGGL(conv_rows_bf16_kernel<true>, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
   else
+#endif
     hipLaunchKernelGGL(conv_rows_bf16_kernel<false>, dim3(grid), dim3(NT), 0, s, a, (int)nstrips);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;

@@ -22,6 +22,13 @@ namespace eosv {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+#ifdef EOSV_PROFILING
+int env_switch(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+#endif
+
 struct Conv {
   int cin = 0, cout = 0, kh = 1, kw = 1, kwp = 1, cinp = 0, stride = 1, pad = 0, K = 0;
   bool stem = false;
@@ -31,6 +38,7 @@ struct Conv {
   std::string wname, bnname;  // state_dict prefixes
   void* w = nullptr;          // [cout][K] (f32 or bf16)
   float* b = nullptr;         // [cout]
+  size_t wbytes = 0;          // size of the w allocation (reused by a reload of the same shape)
 };
 
 struct Block {
@@ -104,10 +112,7 @@ static Conv make_conv(int cin, int cout, int k, int stride, int pad, const std::
 // block's last conv: out = relu(W_last . h + W_ds . x_strided + b_last + b_ds), one launch
 // instead of two and no residual round trip through HBM.  EOSV_FUSE_DS=0: separate launch.
 static bool fuse_ds_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("EOSV_FUSE_DS");
-    return !e || atoi(e) != 0;
-  }();
+  static const bool v = env_switch("EOSV_FUSE_DS", 1) != 0;
   return v;
 }
 
@@ -227,6 +232,19 @@ static int dmalloc(eosv_handle* h, void** p, size_t bytes) {
   return EOSV_OK;
 }
 
+// Copy host bytes into a weight buffer.  The handle's layer shapes are fixed, so a reload
+// (eosv_load_weights called again) overwrites the previous allocation in place instead of
+// allocating a new one: device memory stays constant across reloads.
+static int upload_bytes(eosv_handle* h, void** dst, size_t* cap, const void* src, size_t bytes) {
+  int rc;
+  if (!*dst || *cap != bytes) {
+    if ((rc = dmalloc(h, dst, bytes))) return rc;
+    *cap = bytes;
+  }
+  EOSV_HIP_CHECK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return EOSV_OK;
+}
+
 static unsigned short f2bf_host(float f) {
   unsigned u;
   memcpy(&u, &f, 4);
@@ -337,15 +355,12 @@ static int upload_conv(eosv_handle* h, Conv& c, const Tensors& t, bool bf16, boo
   if (bf16) {
     std::vector<unsigned short> wb(wf.size());
     for (size_t i = 0; i < wf.size(); ++i) wb[i] = f2bf_host(wf[i]);
-    if ((rc = dmalloc(h, &c.w, wb.size() * 2))) return rc;
-    EOSV_HIP_CHECK(hipMemcpy(c.w, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+    if ((rc = upload_bytes(h, &c.w, &c.wbytes, wb.data(), wb.size() * 2))) return rc;
   } else {
-    if ((rc = dmalloc(h, &c.w, wf.size() * 4))) return rc;
-    EOSV_HIP_CHECK(hipMemcpy(c.w, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = upload_bytes(h, &c.w, &c.wbytes, wf.data(), wf.size() * 4))) return rc;
   }
-  if ((rc = dmalloc(h, (void**)&c.b, (size_t)c.cout * 4))) return rc;
-  EOSV_HIP_CHECK(hipMemcpy(c.b, beta.data(), (size_t)c.cout * 4, hipMemcpyHostToDevice));
-  return EOSV_OK;
+  size_t bcap = c.b ? (size_t)c.cout * 4 : 0;
+  return upload_bytes(h, (void**)&c.b, &bcap, beta.data(), (size_t)c.cout * 4);
 }
 
 static hipEvent_t prof_event(eosv_handle* h) {
@@ -389,10 +404,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
     a.K1 = c.K;
   }
   a.zero = h->zero;
-  static const int xcd = [] {
-    const char* e = getenv("EOSV_XCD");  // 0 = plain blockIdx order (A/B switch)
-    return e ? atoi(e) : 1;
-  }();
+  static const int xcd = env_switch("EOSV_XCD", 1);  // 0 = plain blockIdx order (A/B switch)
   a.xcd = xcd;
   a.kcm = c.kcm ? 1 : 0;
   a.split = (bf16 && x3(h)) ? 1 : 0;
@@ -454,14 +466,8 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
 }
 
 static bool stem_pool_fused(bool bf) {
-  static const bool vb = [] {
-    const char* e = getenv("EOSV_BF16_STEMPOOL");  // 0 = separate stem conv + maxpool (A/B switch)
-    return !e || atoi(e) != 0;
-  }();
-  static const bool vf = [] {
-    const char* e = getenv("EOSV_F32_STEMPOOL");  // 0 = separate stem conv + maxpool (A/B switch)
-    return !e || atoi(e) != 0;
-  }();
+  static const bool vb = env_switch("EOSV_BF16_STEMPOOL", 1) != 0;  // 0 = separate stem conv + maxpool (A/B switch)
+  static const bool vf = env_switch("EOSV_F32_STEMPOOL", 1) != 0;  // 0 = separate stem conv + maxpool (A/B switch)
   return bf ? vb : vf;
 }
 
@@ -470,14 +476,8 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
                      bool bf, hipStream_t s) {
   const int H = h->d.height, W = h->d.width;
   int rc;
-  static const bool direct = [] {
-    const char* e = getenv("EOSV_STEM_DIRECT");  // 0 = pack kernel + LDS-DMA rows (A/B switch)
-    return !e || atoi(e) != 0;
-  }();
-  static const bool x3_split_stem = [] {
-    const char* e = getenv("EOSV_X3_STEM");  // 0 = exact-f32 MFMA stem for EOSV_F32X3 (A/B switch)
-    return !e || atoi(e) != 0;
-  }();
+  static const bool direct = env_switch("EOSV_STEM_DIRECT", 1) != 0;  // 0 = pack kernel + LDS-DMA rows (A/B switch)
+  static const bool x3_split_stem = env_switch("EOSV_X3_STEM", 1) != 0;  // 0 = exact-f32 MFMA stem for EOSV_F32X3 (A/B switch)
   const bool sbf = stem_bf(h);  // EOSV_F32X3: split-bf16 (or exact-f32) stem with split output, bf16 blocks
   // EOSV_F32X3: the split-bf16 fused stem reads the f32 frames directly
   const bool x3stem = x3(h) && direct && x3_split_stem && h->stem_x3.w && stem_pool_x3_ok(H, W);
@@ -575,8 +575,7 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->buf[i], F * h->act_elems * elt);
   {
     // front-stage sub-chunk: keeps stem/layer1 activations Infinity-Cache resident
-    const char* e = getenv("EOSV_SUB_FRAMES");
-    int sub = e ? atoi(e) : 0;  // measured: no gain at 64..256 (R18 f32/bf16, R50 bf16)
+    int sub = env_switch("EOSV_SUB_FRAMES", 0);  // measured: no gain at 64..256 (R18 f32/bf16, R50 bf16)
     if (sub > 0 && sub < desc->max_frames) {
       h->sub_frames = sub;
       for (int i = 0; i < 4 && !rc; ++i) rc = dmalloc(h, &h->sbuf[i], (size_t)sub * h->act_elems * elt);
@@ -604,6 +603,8 @@ int eosv_load_weights(eosv_handle* h, const char* const* names, const void* cons
   }
   const bool bf = conv_bf(h), sp = x3(h);
   int rc;
+  // a reload overwrites the weight buffers in place: let every queued forward finish first
+  if (h->loaded) EOSV_HIP_CHECK(hipDeviceSynchronize());
   h->loaded = false;
   if ((rc = upload_conv(h, h->stem, t, stem_bf(h), true))) return rc;
   if (sp) {  // split-bf16 stem weights: the bf16 stem layout (K 192), as hi and lo = bf16(w - hi)
@@ -617,10 +618,12 @@ int eosv_load_weights(eosv_handle* h, const char* const* names, const void* cons
       wb[i] = f2bf_host(hi);
       wb[wf.size() + i] = f2bf_host(wf[i] - hi);
     }
-    if ((rc = dmalloc(h, &c.w, wb.size() * 2))) return rc;
-    EOSV_HIP_CHECK(hipMemcpy(c.w, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
-    if ((rc = dmalloc(h, (void**)&c.b, (size_t)c.cout * 4))) return rc;
-    EOSV_HIP_CHECK(hipMemcpy(c.b, beta.data(), (size_t)c.cout * 4, hipMemcpyHostToDevice));
+    c.w = h->stem_x3.w;
+    c.b = h->stem_x3.b;
+    c.wbytes = h->stem_x3.wbytes;
+    if ((rc = upload_bytes(h, &c.w, &c.wbytes, wb.data(), wb.size() * 2))) return rc;
+    size_t bcap = c.b ? (size_t)c.cout * 4 : 0;
+    if ((rc = upload_bytes(h, (void**)&c.b, &bcap, beta.data(), (size_t)c.cout * 4))) return rc;
     h->stem_x3 = c;
   }
   for (Block& b : h->blocks) {

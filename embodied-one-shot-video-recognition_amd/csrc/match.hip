@@ -1,25 +1,35 @@
 // One-shot matching kernels (the hot-path sink, reference classifier.py / network_test.py).
 //
 //  match_protonet : classifier.py:9-40 + 43-90 -- per-label prototype = sequential f32
-//                   mean in first-appearance order; scipy cdist 'euclidean' in f64 on the
-//                   f32 inputs; torch.FloatTensor (f64->f32); softmax(-d) over the
-//                   prototypes (max-subtract, exp, 1/sum, scale); np.argmax (first max).
+//                   mean in first-appearance order (np.mean over axis 0); scipy cdist
+//                   'euclidean' on the f32 inputs: f64 differences, squared and summed
+//                   SEQUENTIALLY over d = 0..D-1 with separate multiply and add (scipy's loop;
+//                   checked bit-exact, tests/test_cpu_host.py), sqrt, torch.FloatTensor
+//                   (f64 -> f32); softmax(-d) over the prototypes (max-subtract, exp, 1/sum,
+//                   scale); np.argmax (first max).
 //  match_cosine   : classifier.py:117-120 -- sklearn cosine_similarity (rows divided by
 //                   their f32 L2 norm, zero norm -> 1) then argsort(-s)[:,0] = first max.
 //  segment_match  : network_test.py:207-214 + models.py:42-56 -- cdist(seg, gallery) f64
-//                   -> f32 -> 3-tap [l1,l2,l1] conv along the flattened segment axis with
-//                   zero padding -> first argmin over the gallery.
-// One block per episode (matching is < 1% of the path's time); all reductions are
-// fixed-order trees, so results are run-to-run deterministic.
+//                   (sequential, as above) -> f32 -> 3-tap [l1,l2,l1] conv along the flattened
+//                   segment axis with zero padding (torch-CPU's k-ordered FMA chain) -> first
+//                   argmin over the gallery.
+// hipcc contracts a * b + c into an FMA by default (even through __dmul_rn / __dadd_rn): this
+// file turns contraction off, so every product scipy rounds separately is rounded here too;
+// the smoothing's FMAs are explicit fmaf calls (torch-CPU's conv arithmetic).
+// Matching is < 1 % of the path's time; all reductions have a fixed order, so results are
+// run-to-run deterministic.
 #include <cfloat>
 
 #include "common.h"
+
+#pragma clang fp contract(off)
 
 namespace eosv {
 
 constexpr int MT = 256;
 constexpr int MAXV = 8;  // D <= 2048
 constexpr int MAXP = 64;
+constexpr int PG = 8;    // prototypes per LDS group (8 x 2048 f32 = 64 KiB)
 
 template <typename T>
 __device__ __forceinline__ T block_sum(T v, T* red) {
@@ -31,51 +41,57 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// One block per episode.  Prototype means are built in parallel (one thread per dimension,
+// sequential over the support rows) into LDS, PG prototypes at a time; then lane p of wave 0
+// runs prototype p's distance as ONE sequential f64 chain over d, exactly scipy's order.
 __global__ __launch_bounds__(MT) void match_protonet_kernel(
     const float* __restrict__ query, const float* __restrict__ sup, const int* __restrict__ sup_off,
     const int* __restrict__ sup_slot, const int* __restrict__ n_proto, int D, long long* __restrict__ pred,
     float* __restrict__ score) {
-  __shared__ double red[4];
+  __shared__ float qs[MT * MAXV];
+  __shared__ float ps[PG][MT * MAXV];
   __shared__ float dist[MAXP];
   const int e = blockIdx.x;
   const int s0 = sup_off[e], s1 = sup_off[e + 1];
-  const int P = n_proto[e];
+  const int P = min(n_proto[e], MAXP);  // eosv_match documents n_way <= 64
   const int tid = threadIdx.x;
-  float q[MAXV];
+  for (int d = tid; d < D; d += MT) qs[d] = query[(long long)e * D + d];
+  for (int p0 = 0; p0 < P; p0 += PG) {
+    const int np = min(PG, P - p0);
+    for (int g = 0; g < np; ++g) {
+      float acc[MAXV];
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int d = tid + MT * j;
-    q[j] = d < D ? query[(long long)e * D + d] : 0.f;
-  }
-  for (int p = 0; p < P; ++p) {
-    float acc[MAXV];
+      for (int j = 0; j < MAXV; ++j) acc[j] = 0.f;
+      int cnt = 0;
+      for (int s = s0; s < s1; ++s) {
+        if (sup_slot[s] != p0 + g) continue;
+        const float* row = sup + (long long)s * D;
+        // np.mean(axis=0): the first row is copied, the others added in order
 #pragma unroll
-    for (int j = 0; j < MAXV; ++j) acc[j] = 0.f;
-    int cnt = 0;
-    for (int s = s0; s < s1; ++s) {
-      if (sup_slot[s] != p) continue;
-      ++cnt;
-      const float* row = sup + (long long)s * D;
+        for (int j = 0; j < MAXV; ++j) {
+          const int d = tid + MT * j;
+          if (d < D) acc[j] = cnt ? acc[j] + row[d] : row[d];
+        }
+        ++cnt;
+      }
+      const float fc = (float)cnt;
 #pragma unroll
       for (int j = 0; j < MAXV; ++j) {
         const int d = tid + MT * j;
-        if (d < D) acc[j] += row[d];
+        if (d < D) ps[g][d] = acc[j] / fc;
       }
     }
-    double part = 0.0;
-    const float fc = (float)cnt;
-#pragma unroll
-    for (int j = 0; j < MAXV; ++j) {
-      const int d = tid + MT * j;
-      if (d < D) {
-        const double diff = (double)q[j] - (double)(acc[j] / fc);
-        part += diff * diff;
+    __syncthreads();
+    if (tid < np) {
+      double ss = 0.0;
+      for (int d = 0; d < D; ++d) {
+        const double diff = (double)qs[d] - (double)ps[tid][d];
+        ss = ss + diff * diff;
       }
+      dist[p0 + tid] = (float)sqrt(ss);
     }
-    const double ss = block_sum(part, red);
-    if (tid == 0) dist[p] = (float)sqrt(ss);
+    __syncthreads();
   }
-  __syncthreads();
   if (tid == 0) {
     // softmax(-d) as torch-CPU computes it, then np.argmax (first maximum)
     float mx = -INFINITY;
@@ -158,98 +174,89 @@ __global__ __launch_bounds__(MT) void match_cosine_kernel(const float* __restric
 }
 
 // ---------------------------------------------------------------- segment matching
-// dist[s][g] = sqrt(sum_d (seg[s][d] - gal[g][d])^2) in f64, stored f32.
-// Block: 64 gallery rows x up to 64 segment rows, D staged through LDS in chunks of 32.
+// Fused: distances, smoothing and the first argmin in one pass, no [rows, G] scratch.
+// A block owns SG_G gallery columns x SG_S output rows and also computes the rows just above
+// and below (the smoothing halo, recomputed by the neighbouring blocks: +3 %).
+// dist[s][g] = sqrt(sum_d (seg[s][d] - gal[g][d])^2) in f64, summed sequentially over d
+// (d-chunks of SG_DK staged through LDS in order), stored f32; smoothed[s][g] =
+// fma(l1, d[s+1][g], fma(l2, d[s][g], l1 * d[s-1][g])) with zeros outside the row's episode;
+// per row the (value, column) minimum of the block's columns is merged into ids[s] by a 64-bit
+// atomic min on (float bits << 32 | g): the values are >= 0, so their bit patterns order like
+// the floats, and equal values resolve to the smaller g (np.argsort(...)[:, 0] on ties).
 constexpr int SG_G = 64, SG_S = 64, SG_DK = 32;
+constexpr int SG_R = SG_S + 2;             // computed rows (halo included)
+constexpr int SG_RPT = (SG_R + 3) / 4;     // rows per thread (4 row groups of 64 threads)
 
-__global__ __launch_bounds__(256) void seg_dist_kernel(const float* __restrict__ seg, int S,
-                                                       const float* __restrict__ gal, int G, int D,
-                                                       float* __restrict__ dist) {
+__global__ __launch_bounds__(256) void seg_match_kernel(const float* __restrict__ seg, int R, int S,
+                                                        const float* __restrict__ gal, int G, int D, float l1,
+                                                        float l2, unsigned long long* __restrict__ best,
+                                                        float* __restrict__ out) {
   __shared__ float gs[SG_G][SG_DK + 1];
-  __shared__ float ss[SG_S][SG_DK + 1];
+  __shared__ float ss[SG_RPT * 4][SG_DK + 1];
+  __shared__ float dl[SG_RPT * 4][SG_G + 1];
   const int g0 = blockIdx.x * SG_G;
-  const int sb = blockIdx.y * SG_S;
+  const int r0 = blockIdx.y * SG_S - 1;  // local row 0 = global row r0 (the upper halo)
   const int tid = threadIdx.x;
   const int gl = tid & 63;
-  const int sgrp = tid >> 6;  // 4 groups, thread owns s = sgrp + 4*i
-  double acc[SG_S / 4];
+  const int rg = tid >> 6;  // thread owns local rows rg + 4 i
+  double acc[SG_RPT];
 #pragma unroll
-  for (int i = 0; i < SG_S / 4; ++i) acc[i] = 0.0;
+  for (int i = 0; i < SG_RPT; ++i) acc[i] = 0.0;
   for (int d0 = 0; d0 < D; d0 += SG_DK) {
     for (int t = tid; t < SG_G * SG_DK; t += 256) {
       const int r = t / SG_DK, c = t % SG_DK;
       const int g = g0 + r, d = d0 + c;
       gs[r][c] = (g < G && d < D) ? gal[(long long)g * D + d] : 0.f;
-      const int s = sb + r;
-      ss[r][c] = (s < S && d < D) ? seg[(long long)s * D + d] : 0.f;
+    }
+    for (int t = tid; t < SG_RPT * 4 * SG_DK; t += 256) {
+      const int r = t / SG_DK, c = t % SG_DK;
+      const int row = r0 + r, d = d0 + c;
+      ss[r][c] = (row >= 0 && row < R && d < D) ? seg[(long long)row * D + d] : 0.f;
     }
     __syncthreads();
-#pragma unroll 4
-    for (int c = 0; c < SG_DK; ++c) {
+    const int dn = min(SG_DK, D - d0);
+    for (int c = 0; c < dn; ++c) {
       const double gv = (double)gs[gl][c];
 #pragma unroll
-      for (int i = 0; i < SG_S / 4; ++i) {
-        const double df = (double)ss[sgrp + 4 * i][c] - gv;
-        acc[i] += df * df;
+      for (int i = 0; i < SG_RPT; ++i) {
+        const double df = (double)ss[rg + 4 * i][c] - gv;
+        acc[i] = acc[i] + df * df;
       }
     }
     __syncthreads();
   }
-  const int g = g0 + gl;
-  if (g < G) {
 #pragma unroll
-    for (int i = 0; i < SG_S / 4; ++i) {
-      const int s = sb + sgrp + 4 * i;
-      if (s < S) dist[(long long)s * G + g] = (float)sqrt(acc[i]);
+  for (int i = 0; i < SG_RPT; ++i) dl[rg + 4 * i][gl] = (float)sqrt(acc[i]);
+  __syncthreads();
+  const int g = g0 + gl;
+#pragma unroll
+  for (int i = 0; i < SG_RPT; ++i) {
+    const int lr = rg + 4 * i;  // output local rows 1 .. SG_S
+    const int row = r0 + lr;
+    if (lr < 1 || lr > SG_S || row >= R) continue;  // wave-uniform
+    const int sl = row % S;  // row within its episode
+    const float dm = sl > 0 ? dl[lr - 1][gl] : 0.f;
+    const float dp = sl + 1 < S ? dl[lr + 1][gl] : 0.f;
+    const float v = fmaf(l1, dp, fmaf(l2, dl[lr][gl], l1 * dm));
+    if (out && g < G) out[(long long)row * G + g] = v;
+    unsigned long long key = g < G ? ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)g : ~0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long ok = __shfl_xor(key, o, 64);
+      key = ok < key ? ok : key;
     }
+    if (gl == 0) atomicMin(best + row, key);
   }
 }
 
-// smoothed[s][g] = l1*d[s-1][g] + l2*d[s][g] + l1*d[s+1][g] (zero padded at the ends of each
-// episode's S rows), argmin over g; one block per row of the n_episodes*S rows
-__global__ __launch_bounds__(256) void seg_smooth_argmin_kernel(const float* __restrict__ dist, int S,
-                                                                int G, float l1, float l2,
-                                                                long long* __restrict__ ids,
-                                                                float* __restrict__ out) {
-  __shared__ float bvs[4];
-  __shared__ int bis[4];
-  const int s = blockIdx.x;
-  const int sl = s % S;  // row within its episode
-  float bv = INFINITY;
-  int bi = 0x7fffffff;
-  for (int g = threadIdx.x; g < G; g += 256) {
-    const float dm = sl > 0 ? dist[(long long)(s - 1) * G + g] : 0.f;
-    const float d0 = dist[(long long)s * G + g];
-    const float dp = sl + 1 < S ? dist[(long long)(s + 1) * G + g] : 0.f;
-    const float v = fmaf(l1, dp, fmaf(l2, d0, l1 * dm));
-    if (out) out[(long long)s * G + g] = v;
-    if (v < bv) {  // g increases per thread, so '<' keeps the first minimum
-      bv = v;
-      bi = g;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ov < bv || (ov == bv && oi < bi)) {
-      bv = ov;
-      bi = oi;
-    }
-  }
-  if ((threadIdx.x & 63) == 0) {
-    bvs[threadIdx.x >> 6] = bv;
-    bis[threadIdx.x >> 6] = bi;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w)
-      if (bvs[w] < bv || (bvs[w] == bv && bis[w] < bi)) {
-        bv = bvs[w];
-        bi = bis[w];
-      }
-    ids[s] = bi;
-  }
+__global__ void seg_ids_init_kernel(unsigned long long* __restrict__ best, int R) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < R) best[t] = ~0ull;
+}
+
+__global__ void seg_ids_final_kernel(unsigned long long* __restrict__ best, int R) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < R) best[t] &= 0xffffffffull;  // keep the column: ids[s] as int64
 }
 
 __global__ void temporal_smooth_kernel(const float* __restrict__ x, int rows, int cols, float l1, float l2,
@@ -294,6 +301,7 @@ extern "C" int eosv_match(const float* d_query, const float* d_support, const in
   }
   hipStream_t s = (hipStream_t)stream;
   if (kind == EOSV_MATCH_PROTONET) {
+    // n_proto[e] <= 64 (MAXP) is documented in eosv.h; the kernel clamps, it is device data
     if (!d_sup_slot || !d_n_proto) {
       set_error("eosv_match: protonet needs d_sup_slot and d_n_proto");
       return EOSV_ERR_ARG;
@@ -321,18 +329,14 @@ extern "C" int eosv_segment_match_episodes(const float* d_seg, int n_episodes, i
   }
   hipStream_t s = (hipStream_t)stream;
   const int R = n_episodes * S;  // all episodes' rows against the one gallery: a grid that fills the chip
-  float* raw = nullptr;
-  EOSV_HIP_CHECK(hipMallocAsync((void**)&raw, sizeof(float) * (size_t)R * G, s));
+  unsigned long long* best = (unsigned long long*)d_ids;  // the (value, column) keys live in d_ids
+  const unsigned nb = (unsigned)((R + 255) / 256);
+  hipLaunchKernelGGL(seg_ids_init_kernel, dim3(nb), dim3(256), 0, s, best, R);
   dim3 grid((G + SG_G - 1) / SG_G, (R + SG_S - 1) / SG_S);
-  hipLaunchKernelGGL(seg_dist_kernel, grid, dim3(256), 0, s, d_seg, R, d_gallery, G, D, raw);
-  hipLaunchKernelGGL(seg_smooth_argmin_kernel, dim3(R), dim3(256), 0, s, raw, S, G, lamda1, lamda2,
-                     (long long*)d_ids, d_dist);
-  const hipError_t le = hipGetLastError();
-  EOSV_HIP_CHECK(hipFreeAsync(raw, s));
-  if (le != hipSuccess) {
-    set_error(std::string("eosv_segment_match launch: ") + hipGetErrorString(le));
-    return EOSV_ERR_HIP;
-  }
+  hipLaunchKernelGGL(seg_match_kernel, grid, dim3(256), 0, s, d_seg, R, S, d_gallery, G, D, lamda1, lamda2, best,
+                     d_dist);
+  hipLaunchKernelGGL(seg_ids_final_kernel, dim3(nb), dim3(256), 0, s, best, R);
+  EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
 

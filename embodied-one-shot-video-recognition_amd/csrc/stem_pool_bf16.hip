@@ -738,10 +738,7 @@ int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w,
 }
 
 static bool stem_cb() {
-  static const bool v = [] {
-    const char* e = getenv("EOSV_STEM_CB");  // 0 = full-width workgroups (A/B switch)
-    return !e || atoi(e) != 0;
-  }();
+  static const bool v = env_switch("EOSV_STEM_CB", 1) != 0;  // 0 = full-width workgroups (A/B switch)
   return v;
 }
 

@@ -10,7 +10,9 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libeosv.so")
+# EOSV_LIBRARY selects another build of the same ABI: tools/ set it to libeosv_prof.so (the
+# profiling build with the A/B switches and ablations compiled in, `make -C csrc prof`)
+LIB_PATH = os.environ.get("EOSV_LIBRARY") or os.path.join(PKG_ROOT, "libeosv.so")
 
 EOSV_F32, EOSV_BF16, EOSV_F32X3 = 0, 1, 2
 MATCH_PROTONET, MATCH_COSINE = 0, 1

@@ -361,7 +361,9 @@ class TestNetwork():
                 slots += [sl_] * (ns_v + 1)
             nproto.append(len(seen))
             off.append(off[-1] + nk * (ns_v + 1))
-        kind = self.classifier if self.classifier in ('protonet', 'cosine') else 'protonet'
+        kind = self.classifier if self.classifier in ('protonet', 'cosine') else None
+        if kind is None:
+            raise NotImplementedError(f"classifier {self.classifier!r} is outside the GPU path")
         pred, _ = _engine.match(q_emb, sup.contiguous(), t(off), t(slots), t(nproto), kind)
         if debug is not None:
             debug.update(seg=seg, pool=pool, sup=sup, q_emb=q_emb, pred=pred)

@@ -40,7 +40,8 @@ typedef enum { EOSV_ARCH_R18 = 18, EOSV_ARCH_R50 = 50, EOSV_ARCH_R101 = 101 } eo
 /* EOSV_F32X3: f32-accurate split-bf16 arithmetic.  Activations are stored as bf16 (hi, lo)
  * pairs (hi = bf16(v), lo = bf16(v - hi): 16 significant bits), weights likewise, and every
  * conv sums the three bf16 MFMA products hi.hi + lo.hi + hi.lo in f32 ("bf16x3"): ~2^-16
- * relative per product, against 2^-8 for plain bf16.  The stem stays exact f32. */
+ * relative per product, against 2^-8 for plain bf16.  The fused stem + maxpool uses the same
+ * split (frames and weights as hi + lo, three bf16 MFMAs per k-slice). */
 typedef enum { EOSV_F32 = 0, EOSV_BF16 = 1, EOSV_F32X3 = 2 } eosv_dtype;
 typedef enum { EOSV_MATCH_PROTONET = 0, EOSV_MATCH_COSINE = 1 } eosv_match_kind;
 
@@ -93,9 +94,12 @@ int eosv_segment_mean(const float* d_feat, int n_seg, int seg_len, int D, float*
  *   d_sup_off  [n_episodes+1]       int32 row offsets into d_support
  *   d_sup_slot [sum S_e]            int32 prototype slot of each support row
  *                                   (first-appearance order of its label, classifier.py:20-36)
- *   d_n_proto  [n_episodes]         int32 prototypes per episode (<= 64)
- * kind = PROTONET: f64 cdist to per-slot means -> f32 -> softmax(-d) -> argmax
- *        (classifier.py:43-90); d_pred = prototype position, d_score = distances.
+ *   d_n_proto  [n_episodes]         int32 prototypes per episode (n_way <= 64; larger
+ *                                   values are clamped to 64 on the device)
+ * kind = PROTONET: f64 cdist to per-slot means (scipy's sequential f64 sum, no fused
+ *        multiply-add: distances bit-identical to classifier.py:63 on the same features)
+ *        -> f32 -> softmax(-d) -> argmax (classifier.py:43-90); d_pred = prototype position,
+ *        d_score = the f32 distances (the top-2 margin of an episode is read from them).
  * kind = COSINE:   cosine similarity to every support row -> argmax (classifier.py:117-120);
  *        d_pred = support row index within the episode, d_score = similarities.
  * d_score [n_episodes, max_cols] f32 (may be NULL), max_cols = 64. */
@@ -106,7 +110,8 @@ int eosv_match(const float* d_query, const float* d_support, const int32_t* d_su
 /* Config-3 gallery matching (network_test.py:207-214 + models.py:42-56):
  * dist = cdist(d_seg [S,D], d_gallery [G,D]) in f64 -> f32 -> 3-tap smoothing
  * [l1,l2,l1] along the S axis with zero padding -> first argmin over G per row.
- * d_ids [S] int64; d_dist [S,G] f32 smoothed distances (may be NULL). */
+ * d_ids [S] int64; d_dist [S,G] f32 smoothed distances (may be NULL).  One fused pass: no
+ * device allocation, no [S,G] scratch (d_ids doubles as the per-row argmin accumulator). */
 int eosv_segment_match(const float* d_seg, int S, const float* d_gallery, int G, int D,
                        float lamda1, float lamda2, int64_t* d_ids, float* d_dist,
                        eosv_stream_t stream);

@@ -1,5 +1,7 @@
 #!/bin/bash
 # A/B an environment switch on the bench: VAR=<env var> VALS="<v1> <v2> ..." [DTYPE=bf16] [ARCH=resnet18]
+# (A/B switches exist only in the profiling build: `make -C embodied-one-shot-video-recognition_amd/csrc prof`)
+export EOSV_LIBRARY="${EOSV_LIBRARY:-$PWD/embodied-one-shot-video-recognition_amd/libeosv_prof.so}"
 # [ROUNDS=2] [BENCH_EXTRA=...]. Interleaved rounds; per-layer timings of the last round printed side by side.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

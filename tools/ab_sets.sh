@@ -1,5 +1,7 @@
 #!/bin/bash
 # A/B sets of env assignments on the bench (per-layer times of layers $LAYERS):
+# (A/B switches exist only in the profiling build: `make -C embodied-one-shot-video-recognition_amd/csrc prof`)
+export EOSV_LIBRARY="${EOSV_LIBRARY:-$PWD/embodied-one-shot-video-recognition_amd/libeosv_prof.so}"
 #   SETS="EOSV_A=1 EOSV_B=2;EOSV_A=0" [DTYPE=bf16] [CHECK=1: run tests/native/conv_check under each set first]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

@@ -1,5 +1,7 @@
 #!/bin/bash
 # f32x3 split-bf16 stem: native checks + f32x3 parity tests, then stem A/B (EOSV_X3_STEM)
+# (A/B switches exist only in the profiling build: `make -C embodied-one-shot-video-recognition_amd/csrc prof`)
+export EOSV_LIBRARY="${EOSV_LIBRARY:-$PWD/embodied-one-shot-video-recognition_amd/libeosv_prof.so}"
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 120 tests/native/conv_check > gpurun_out/conv_check.log 2>&1; rc=$?

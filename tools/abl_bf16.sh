@@ -1,5 +1,7 @@
 #!/bin/bash
 # bf16 conv ablations (EOSV_CONV_ABL bits: 1 no main-loop loads, 4 no A, 8 no B, 2 no stores).
+# (A/B switches exist only in the profiling build: `make -C embodied-one-shot-video-recognition_amd/csrc prof`)
+export EOSV_LIBRARY="${EOSV_LIBRARY:-$PWD/embodied-one-shot-video-recognition_amd/libeosv_prof.so}"
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for abl in ${ABLS:-0 1 4 8 2}; do

@@ -1,5 +1,7 @@
 #!/bin/bash
 # GPU-side (rocprofv3) durations of ablated bf16 conv kernels: EOSV_CONV_ABL values in $ABLS
+# (A/B switches exist only in the profiling build: `make -C embodied-one-shot-video-recognition_amd/csrc prof`)
+export EOSV_LIBRARY="${EOSV_LIBRARY:-$PWD/embodied-one-shot-video-recognition_amd/libeosv_prof.so}"
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 for A in ${ABLS:-113}; do
