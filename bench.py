@@ -62,11 +62,14 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args, episodes, T):
-    """Oracle (fp32 torch-CPU restatement of the reference path) on a bounded sample."""
+def cpu_baseline(args, batch, T, emb, preds):
+    """Oracle (fp32 torch-CPU restatement of the reference path) on a bounded sample of the last
+    timed step's episodes; also checks the GPU leg against it on that sample (``cpu_parity``):
+    predictions, clip embeddings, and the top-2 distance margin of every sampled episode."""
     sys.path.insert(0, REPO)
     from eosv import arch as arch_mod, synth  # noqa
     from oracle import harness_ref, resnet_ref  # noqa  (checker / CPU baseline only)
+    from scipy.spatial.distance import cdist
 
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
@@ -80,25 +83,44 @@ def cpu_baseline(args, episodes, T):
 
     t_load = 0.0
     clips = frames = done = 0
+    pred_equal, emb_rel, margins = 0, 0.0, []
     t0 = time.perf_counter()
-    for ep in episodes:
+    for j, ep in enumerate(batch.episodes):
         tl = time.perf_counter()
         vids = [load(v, True) for v in ep["support"]] + [load(ep["query"], False)]
         t_load += time.perf_counter() - tl
         sx = [v for v, _ in vids[:-1]]
         sf = [n for _, n in vids[:-1]]
-        harness_ref.epoch_features(model, sx, True, sf)
-        harness_ref.epoch_features(model, [vids[-1][0]], True)
+        s_emb = harness_ref.epoch_features(model, sx, True, sf)
+        q_emb = harness_ref.epoch_features(model, [vids[-1][0]], True)
         clips += len(vids)
         frames += sum(n for _, n in vids)
         done += 1
+        tc = time.perf_counter()
+        # checker (excluded from the CPU time like the frame generation)
+        sy = np.array(ep["support_y"], np.float32)
+        ref_pred = harness_ref.protonet_predict(s_emb, sy, q_emb, np.array([ep["query_y"]], np.float32))[0][0]
+        pred_equal += int(ref_pred == int(preds[j]))
+        s0, s1 = int(batch.sup_off[j]), int(batch.sup_off[j + 1])
+        got = np.concatenate([emb[s0:s1], emb[batch.n_support + j][None]])
+        ref = np.concatenate([s_emb, q_emb])
+        emb_rel = max(emb_rel, float((np.abs(got - ref).max(1) / np.abs(ref).max(1)).max()))
+        _, protos = harness_ref.prototypes(s_emb, sy)
+        d = np.sort(cdist(q_emb.astype(np.float64), protos.astype(np.float64))[0])
+        margins.append((d[1] - d[0]) / d[0])
+        t_load += time.perf_counter() - tc
         if time.perf_counter() - t0 - t_load > args.cpu_baseline_sec:
             break
     el = time.perf_counter() - t0 - t_load
-    return {"value": round(clips / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
-            "sample": f"{done} episodes ({clips} clips, {frames} frames) of the same workload through "
+    base = {"value": round(clips / el, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"{done} episodes ({clips} clips, {frames} frames) of the last timed step through "
                       f"oracle/ (torch-CPU fp32 restatement of network_test.py:49-68 + classifier.py), "
-                      f"synthetic-frame generation excluded; {el:.1f}s"}
+                      f"synthetic-frame generation and the parity check excluded; {el:.1f}s"}
+    parity = {"episodes": done, "pred_equal": pred_equal, "max_emb_rel": float(f"{emb_rel:.3g}"),
+              "min_top2_margin": float(f"{min(margins):.3g}"),
+              "near_ties": int(sum(m < 1e-5 for m in margins)),
+              "against": f"{args.dtype} leg, last timed step"}
+    return base, parity
 
 
 def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
@@ -191,11 +213,36 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
     return out
 
 
+def spawn_ranks(n):
+    """``--gpus N`` without a launcher: start N rank processes (RANK / LOCAL_RANK / WORLD_SIZE,
+    rendezvous on 127.0.0.1) and wait for them.  This process never touches the GPU (no HIP
+    call happens before here), and the ranks are children, not an exec of this process.
+    Rank 0 prints the JSON line; the exit code is the first failing rank's."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} ranks", file=sys.stderr)
+    # one rank per GPU; more ranks than devices share them round-robin (gloo rehearsals only)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = world > 1
     torch.cuda.set_device(local)
     if dist:
@@ -250,8 +297,9 @@ def main():
         rl["flop_per_frame"] = round(gflop_frame * 1e9)
         out = {
             "metric": "clips/sec/GPU (224\u00b2, 8-seg) + 5-way-1-shot episode acc vs reference",
-            "value": round(clips / elapsed, 2),
+            "value": round(clips / elapsed, 2),  # whole job: all ranks' clips / max-over-ranks time
             "unit": "clips/s",
+            "value_per_gpu": round(clips / elapsed / world, 2),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -277,7 +325,8 @@ def main():
         if args.layers:
             print_layers(prof, args.dtype)
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, [plans[e] for e in mine_idx[:50]], T)
+            last = batches[-1].batch
+            out["cpu_baseline"], out["cpu_parity"] = cpu_baseline(args, last, T, emb, pred[-len(last.episodes):].cpu().numpy())
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

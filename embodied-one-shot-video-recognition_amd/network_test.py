@@ -213,6 +213,9 @@ class TestNetwork():
         if kind is None:
             raise NotImplementedError(f"classifier {self.classifier!r} is outside the GPU path")
         pred, _ = _engine.match(emb[ns:].contiguous(), emb[:ns].contiguous(), t(sup_off), t(slots), t(nproto), kind)
+        debug = getattr(self, 'debug', None)
+        if debug is not None:  # tests: per-batch clip embeddings (supports, then queries)
+            debug.setdefault('batches', []).append(dict(sup=emb[:ns], q=emb[ns:], sup_off=sup_off, pred=pred))
         return pred.cpu().tolist()
 
     def _baseline_per_episode(self, n):

@@ -52,6 +52,8 @@ from eosv import synth, arch  # noqa: E402  (input generator only)
 from oracle.resnet_ref import torchvision_resnet  # noqa: E402
 
 H = W = 224
+SHAPE = {"H": H, "W": W}  # frame size the ToTensor stub produces (configs 4/5 change it)
+C5_SEED = 39  # the first seed whose 2 config-5 episodes have no video shorter than T = 64
 
 
 # ----------------------------------------------------------------------------- stubs
@@ -99,7 +101,7 @@ def _install_stubs():
     class ToTensor:
         def __call__(self, img):
             cls = img.video_info.split("/")[0]
-            return torch.from_numpy(synth.synth_frame(cls, img.video_info, img.fid, H, W))
+            return torch.from_numpy(synth.synth_frame(cls, img.video_info, img.fid, SHAPE["H"], SHAPE["W"]))
 
     class Normalize:
         def __init__(self, mean, std):
@@ -313,15 +315,164 @@ def capture_aug(mods, seed, episodes, tag):
     print(tag, "acc", acc_text.strip().splitlines()[-1])
 
 
+class episode_shape:
+    """Run the reference at another episode shape, the way its users do: by editing the
+    globals of utils.py (n_way / k_shot / VIDEO_FRAMES / TEST_LIST, utils.py:17-35).
+
+    ``from utils import *`` copied n_way / k_shot / TEST_LIST into episode_novel_dataloader's
+    namespace, and the loaders bound ``video_frames=VIDEO_FRAMES`` as a default at definition
+    time (utils.py:97, 171, 215), so those copies and defaults are set too; ``_3``'s frame count
+    reads the global (utils.py:257).  ``res`` is the frame size the ToTensor stub produces."""
+
+    def __init__(self, mods, n_way=5, k_shot=1, T=16, test_list=None, res=224):
+        self.mods, self.new = mods, dict(n_way=n_way, k_shot=k_shot, T=T, test_list=test_list, res=res)
+
+    def _apply(self, n_way, k_shot, T, test_list, res):
+        u, edl = self.mods["utils"], self.mods["edl"]
+        for m in (u, edl):
+            m.n_way, m.k_shot = n_way, k_shot
+            m.TEST_LIST = test_list
+        u.VIDEO_FRAMES = T
+        for f in (u.get_video_from_video_info, u.get_video_from_video_info_2, u.get_video_from_video_info_3):
+            f.__defaults__ = (T,) + f.__defaults__[1:]
+        SHAPE["H"] = SHAPE["W"] = res
+
+    def __enter__(self):
+        u = self.mods["utils"]
+        self.old = dict(n_way=u.n_way, k_shot=u.k_shot, T=u.VIDEO_FRAMES, test_list=u.TEST_LIST, res=SHAPE["H"])
+        new = dict(self.new)
+        new["test_list"] = new["test_list"] or self.old["test_list"]
+        self._apply(**new)
+
+    def __exit__(self, *a):
+        self._apply(**self.old)
+
+
+def _proto_dists(p):
+    """cdist(query, prototypes) in f64 exactly as classifier.py:17-63 builds it."""
+    from scipy.spatial.distance import cdist
+
+    protos, ids = [], {}
+    for f, y in zip(p["support_feature"], p["support_y"]):
+        ids.setdefault(float(y), []).append(f)
+    protos = np.array([np.mean(np.array(v), axis=0) for v in ids.values()])
+    return cdist(np.asarray(p["query_feature"]), protos, metric="euclidean")[0]
+
+
+def capture_shaped(mods, arch_name, kind, seed, episodes, tag, n_way, k_shot, T, test_list=None,
+                   res=224, backbone=None, features=True):
+    """test_network_baseline at a non-default episode shape (configs 4 / 5), or a long
+    predictions-only run (features=False: per-episode distances + a feature projection instead
+    of the features).  backbone: the torchvision structure the reference's model_resnet50
+    wraps (``resnet101`` for config 5; the reference has no R101 wrapper, models.py:24-37, so
+    torchvision.models.resnet50 is pointed at the R101 structure and the state_dict is R101's)."""
+    tvm = sys.modules["torchvision.models"]
+    old_r50 = tvm.resnet50
+    if backbone:
+        tvm.resnet50 = lambda pretrained=False: torchvision_resnet(backbone)
+    rec = Recorder(mods)
+    mods["utils"].EPISODE_NUMS["test"] = episodes
+    lst = os.path.join(OUT, test_list) if test_list else None
+    try:
+        with episode_shape(mods, n_way, k_shot, T, lst, res), tempfile.TemporaryDirectory() as td:
+            pkl = os.path.join(td, "model.pkl")
+            _save_state_dict(backbone or arch_name, pkl)
+            acc_path = os.path.join(td, "acc.txt")
+            random.seed(seed)
+            np.random.seed(seed)
+            tn = mods["nt"].TestNetwork(acc_path, arch_name, kind, True)
+            with contextlib_redirect():
+                tn.test_network_baseline(pre_model=pkl)
+            tn.acc_file.close()
+            acc_text = open(acc_path).read()
+    finally:
+        tvm.resnet50 = old_r50
+    eps = split_episodes(rec.calls, n_way * k_shot)
+    assert len(eps) == episodes == len(rec.predicts)
+    for e, p in zip(eps, rec.predicts):
+        e["support_y"] = p["support_y"].astype(int).tolist()
+        e["query_y"] = int(p["query_y"][0])
+    pred = np.stack([p["pred"] for p in rec.predicts]).astype(np.int64)
+    meta = dict(arch=backbone or arch_name, reference_wrapper=arch_name, classifier=kind, seed=seed, L2=True,
+                n_way=n_way, k_shot=k_shot, video_frames=T, H=res, W=res,
+                test_list=test_list or "sources/data/test.list", episodes=eps)
+    if features:
+        np.savez_compressed(os.path.join(OUT, f"{tag}.npz"),
+                            support_feature=np.stack([p["support_feature"] for p in rec.predicts]),
+                            query_feature=np.stack([p["query_feature"] for p in rec.predicts]),
+                            pred=pred)
+        meta["acc_file"] = acc_text
+    else:
+        import hashlib
+
+        dists = np.stack([_proto_dists(p) for p in rec.predicts])
+        srt = np.sort(dists, axis=1)
+        rng = np.random.default_rng(20261016)
+        r = rng.standard_normal(np.asarray(rec.predicts[0]["query_feature"]).shape[-1])
+        proj = np.stack([np.concatenate([np.asarray(p["support_feature"], np.float64) @ r,
+                                         np.asarray(p["query_feature"], np.float64) @ r])
+                         for p in rec.predicts])
+        np.savez_compressed(os.path.join(OUT, f"{tag}.npz"), pred=pred[:, 0], dists=dists,
+                            margin=(srt[:, 1] - srt[:, 0]) / srt[:, 0], proj=proj, proj_vector_seed=20261016)
+        meta["acc_file_sha256"] = hashlib.sha256(acc_text.encode()).hexdigest()
+        meta["acc_file_tail"] = acc_text.splitlines()[-1]
+        pin_plans_to_fixture(meta)
+    with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
+        json.dump(meta, f, indent=None if not features else 1)
+    print(tag, "acc", acc_text.strip().splitlines()[-1])
+
+
+def pin_plans_to_fixture(meta, plans_tag="plans_test_seed0"):
+    """A long predictions-only run at seed 0 draws exactly the 1000-episode plan fixture's
+    episodes (test-mode loading draws nothing from the RNG): check that, then refer to it
+    instead of storing the plans twice."""
+    ref = json.load(open(os.path.join(OUT, plans_tag + ".json")))["episodes"]
+    eps = meta.pop("episodes")
+    assert meta["seed"] == 0 and len(eps) <= len(ref)
+    for e, r in zip(eps, ref):
+        assert (e["support"], e["query"], e["support_y"], e["query_y"]) == \
+            (r["support"], r["query"], r["support_y"], r["query_y"])
+    meta["plans"] = plans_tag + ".json"
+    meta["n_episodes"] = len(eps)
+
+
+def make_unreal14_list(path):
+    """An UnrealAction-shaped novel split (README.md:23-26: 14 actions, 10 real target videos
+    each), in the reference's ``class/video`` list format; names are synthetic."""
+    with open(path, "w") as f:
+        for c in range(14):
+            for v in range(10):
+                f.write(f"unreal_action_{c:02d}/real_target_{c:02d}_{v:03d}\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--aug", action="store_true", help="also capture the (slow) config-3 path")
     ap.add_argument("--only-aug", action="store_true")
+    ap.add_argument("--shapes", action="store_true", help="only the config-4 / config-5 shaped episodes")
+    ap.add_argument("--preds", type=int, default=0, help="only the N-episode predictions fixture (config 2)")
     args = ap.parse_args()
     torch.set_num_threads(8)
     _install_stubs()
     gallery_path = os.path.join(tempfile.mkdtemp(), "gallery.list")
     mods = _import_reference(gallery_path)
+    if args.preds:
+        capture_shaped(mods, "resnet18", "protonet", seed=0, episodes=args.preds, tag=f"c2_r18_preds{args.preds}_seed0",
+                       n_way=5, k_shot=1, T=16, features=False)
+        return
+    if args.shapes:
+        make_unreal14_list(os.path.join(OUT, "unreal14.list"))
+        # config 4: 14-way 1-shot, 16 segments (T = 32), R50 over the UnrealAction-shaped split
+        capture_shaped(mods, "resnet50", "protonet", seed=7, episodes=3, tag="c4_r50_14w1s_t32_seed7",
+                       n_way=14, k_shot=1, T=32, test_list="unreal14.list")
+        # config 5: 5-way 5-shot, 32 segments (T = 64) at 256x256.  Seed C5_SEED's two episodes hold no
+        # video shorter than T: the reference zero-pads short videos with 224x224 frames
+        # (utils.py:252) and its torch.stack fails at any other size.
+        capture_shaped(mods, "resnet50", "protonet", seed=C5_SEED, episodes=2, tag=f"c5_r50_5w5s_t64_256_seed{C5_SEED}",
+                       n_way=5, k_shot=5, T=64, res=256)
+        capture_shaped(mods, "resnet50", "protonet", seed=C5_SEED, episodes=1, tag=f"c5_r101_5w5s_t64_256_seed{C5_SEED}",
+                       n_way=5, k_shot=5, T=64, res=256, backbone="resnet101")
+        return
     if not args.only_aug:
         capture_plans(mods, seed=0, episodes=1000, tag="plans_test_seed0")
         capture_baseline(mods, "resnet18", "protonet", seed=1, episodes=20, tag="c1_r18_protonet_seed1")

@@ -215,3 +215,53 @@ def test_crop_normalize_rejects_bad_window():
     assert L.eosv_crop_normalize_frames(None, 1, 240, 320, 224, 0, -1, 0, m, m, None, None) == -1
     assert b"window" in L.eosv_last_error()
     assert L.eosv_normalize_frames(None, 1, 200, 320, 224, m, m, None, None) == -1  # H < crop
+
+
+# ----------------------------------------------------------------- host AddressSanitizer build
+ASAN_BIN = os.path.join(REPO, "tests", "native", "asan_host")
+
+
+def _asan_bin():
+    src = os.path.join(REPO, "embodied-one-shot-video-recognition_amd", "csrc")
+    subprocess.run(["make", "-s", "-C", src, "asan", "-j", str(min(8, os.cpu_count() or 4))], check=True,
+                   capture_output=True)
+    return ASAN_BIN
+
+
+def test_asan_host_argument_validation():
+    """the C++ glue under AddressSanitizer (+ LeakSanitizer): every entry point's argument
+    checks return an error with a message and touch no memory they do not own."""
+    r = subprocess.run([_asan_bin(), "args"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "asan_host args: ok" in r.stdout
+
+
+@pytest.mark.parametrize("n_way,k_shot,seed,n,sizes", [
+    (5, 1, 0, 200, None),                       # the test split, reference shape
+    (14, 1, 7, 50, [10] * 14),                  # UnrealAction-shaped: every class every episode
+    (5, 5, 39, 40, None),                       # config 5's 5-shot
+    (20, 3, 2 ** 40 + 1, 30, None),             # pool strategy of random.sample
+    (3, 2, 5, 10, [3, 2, 4, 3]),                # a class too small for the query draw -> error
+])
+def test_asan_host_plan_service_matches_library(n_way, k_shot, seed, n, sizes):
+    """The plan service under ASan prints the same plans as the release library's (ctypes)."""
+    if sizes is None:
+        idx = episodes.class_index(episodes.read_list("test"))
+        sizes = [len(v) for v in idx.values()]
+    r = subprocess.run([_asan_bin(), "plan", str(n_way), str(k_shot), str(seed), str(n), *map(str, sizes)],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    import numpy as np
+
+    cls = np.zeros((n, n_way), np.int32)
+    q = np.zeros((n, 2), np.int32)
+    sup = np.zeros((n, n_way, max(k_shot, 1)), np.int32)
+    arr = np.array(sizes, np.int32)
+    rc = _lib.lib().eosv_plan_episodes(arr.ctypes.data, len(sizes), n_way, k_shot, ctypes.c_uint64(seed), n,
+                                       cls.ctypes.data, q.ctypes.data, sup.ctypes.data)
+    if rc:
+        assert r.stdout.startswith(f"ERR {rc} ")
+        return
+    want = " ".join(" ".join(map(str, [*cls[e], *q[e], *sup[e].reshape(-1)[:n_way * k_shot]])) for e in range(n))
+    assert r.stdout.split() == want.split()

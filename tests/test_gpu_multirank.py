@@ -1,0 +1,93 @@
+"""GPU: the episode-sharded multi-rank paths with 2 ranks on the box's
+one device.  RCCL refuses two ranks on one GPU, so these run the same code over gloo
+(EOSV_DIST_BACKEND=gloo); on a node, the driver's N-GPU bench uses RCCL over xGMI.
+
+* the drop-in TestNetwork.test_network_baseline over 2 ranks writes the reference's result file
+  byte for byte (network_test.py:132-167);
+* ``bench.py --gpus 2`` spawns its own ranks (no launcher), reports n_gpus = 2 and the same
+  episode accuracy as the 1-rank run over the same timed episodes.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from _common import load_fixture
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "embodied-one-shot-video-recognition_amd")
+
+_DROPIN = r"""
+import os, random, sys
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+import network_test, utils
+from eosv import arch, synth
+tag, out = sys.argv[3], sys.argv[4]
+import json
+meta = json.load(open(os.path.join(sys.argv[2], "tests", "golden", tag + ".json")))
+utils.EPISODE_NUMS["test"] = len(meta["episodes"])
+pkl = out + ".model.pkl"
+if dist.get_rank() == 0:
+    sd = synth.synth_state_dict(arch.SPECS[meta["arch"]], 64, 0)
+    torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, pkl)
+dist.barrier()
+random.seed(meta["seed"])
+tn = network_test.TestNetwork(out, meta["arch"], meta["classifier"], True)
+tn.episodes_per_batch = 4
+tn.test_network_baseline(pre_model=pkl)
+if dist.get_rank() == 0:
+    tn.acc_file.close()
+dist.destroy_process_group()
+"""
+
+
+def _spawn(argv, world, port, env_extra=None, timeout=240):
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), **(env_extra or {}))
+        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=timeout) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
+    return outs
+
+
+@pytest.mark.parametrize("tag", ["c1_r18_protonet_seed1", "c1_r18_cosine_seed2"])
+def test_dropin_baseline_two_ranks_writes_reference_file(tag, tmp_path):
+    script = tmp_path / "dropin.py"
+    script.write_text(_DROPIN)
+    out = str(tmp_path / "acc.txt")
+    _spawn([sys.executable, str(script), PKG, REPO, tag, out], 2, 29611 + os.getpid() % 500)
+    meta, _ = load_fixture(tag)
+    assert open(out).read() == meta["acc_file"]
+
+
+def _bench(extra_env, gpus, eps):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--steps", "1", "--warmup", "1",
+           "--episodes-per-step", str(eps), "--max-frames", "512", "--no-cpu-baseline", "--secondary-dtype", ""]
+    env = dict(os.environ, **extra_env)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # one JSON line, from rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_ranks_and_matches_one_rank():
+    two = _bench({"EOSV_DIST_BACKEND": "gloo"}, 2, 12)
+    one = _bench({}, 1, 24)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["episodes_timed"] == one["config"]["episodes_timed"] == 24
+    assert two["config"]["parallelism"] == "episode-sharded dp2"
+    # same 24 timed episodes (plans are drawn once in the reference's order and dealt e % world)
+    assert two["episode_acc"] == one["episode_acc"]
+    assert abs(two["value_per_gpu"] * 2 - two["value"]) < 0.02 * two["value"]
