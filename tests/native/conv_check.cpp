@@ -12,11 +12,17 @@ using namespace eosv;
 
 static float frand(unsigned& s) { s = s * 1664525u + 1013904223u; return ((s >> 8) & 0xffff) / 32768.f - 1.f; }
 
-static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int pad, bool stem, bool res, bool relu) {
+// ds_cin > 0: a fused 1x1 stride-2 downsample (ConvArgs::x2) reads x2 [N][2H][2W][ds_cin] into K
+// columns [K1, K1 + ds_cin).  tol: bound on |err| / (1 + sum of |terms|) -- f32 rounding of a
+// K-term dot product grows with the magnitudes summed, not with the (cancelling) result.
+static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int pad, bool stem, bool res, bool relu,
+                 int ds_cin = 0, double tol = 1e-5) {
   // stem: dense padded RGB input [N][H+2p][Wp][3] (zero borders), K = [kh][24] padded to 16
   const int KWp = stem ? 8 : K, Cinp = Cin;
   const int Ho = (H + 2 * pad - K) / stride + 1, Wo = (W + 2 * pad - K) / stride + 1;
-  const int Kd = stem ? (K * 24 + 15) / 16 * 16 : K * KWp * Cinp;
+  const int K1 = stem ? (K * 24 + 15) / 16 * 16 : K * KWp * Cinp;
+  const int Kd = K1 + ds_cin;
+  const int H2 = 2 * Ho, W2 = 2 * Wo;
   const int Hx = stem ? H + 2 * pad : H, Wx = stem ? stem_row_pixels(W, pad) : W, off = stem ? pad : 0;
   unsigned s = 12345;
   std::vector<float> x(stem ? stem_input_elems(N, H, W, pad) : (size_t)N * H * W * Cinp, 0.f),
@@ -31,6 +37,15 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
         for (int c = 0; c < Cin; ++c) w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c] = frand(s);
   for (auto& v : b) v = frand(s);
   for (auto& v : r) v = frand(s);
+  std::vector<float> x2((size_t)N * H2 * W2 * ds_cin);
+  for (auto& v : x2) v = frand(s);
+  for (int o = 0; o < Cout; ++o)
+    for (int c = 0; c < ds_cin; ++c) w[(size_t)o * Kd + K1 + c] = frand(s);
+  float* dx2 = nullptr;
+  if (ds_cin) {
+    hipMalloc(&dx2, x2.size() * 4);
+    hipMemcpy(dx2, x2.data(), x2.size() * 4, hipMemcpyHostToDevice);
+  }
   float *dx, *dw, *db, *dr, *dy;
   hipMalloc(&dx, x.size() * 4); hipMalloc(&dw, w.size() * 4); hipMalloc(&db, b.size() * 4);
   hipMalloc(&dr, r.size() * 4); hipMalloc(&dy, r.size() * 4);
@@ -43,6 +58,9 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
   a.N = N; a.H = H; a.W = W; a.Cin = Cinp; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KH = K; a.KW = K; a.KWp = KWp; a.stride = stride; a.pad = pad; a.K = Kd; a.relu = relu;
   void* dz; hipMalloc(&dz, 256); hipMemset(dz, 0, 256); a.zero = dz;
+  if (ds_cin) {
+    a.x2 = dx2; a.H2 = H2; a.W2 = W2; a.Cin2 = ds_cin; a.stride2 = 2; a.K1 = K1;
+  }
   int rc = launch_conv_f32(a, 0);
   hipDeviceSynchronize();
   std::vector<float> y(r.size());
@@ -52,25 +70,36 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
     for (int oh = 0; oh < Ho; ++oh)
       for (int ow = 0; ow < Wo; ++ow)
         for (int o = 0; o < Cout; ++o) {
-          double acc = b[o];
+          double acc = b[o], sabs = fabs(b[o]);
           for (int kh = 0; kh < K; ++kh)
             for (int kw = 0; kw < K; ++kw) {
               int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
               if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-              for (int c = 0; c < Cin; ++c)
-                acc += (double)x[(((size_t)n * Hx + ih + off) * Wx + iw + off) * Cinp + c] * w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c];
+              for (int c = 0; c < Cin; ++c) {
+                const double t = (double)x[(((size_t)n * Hx + ih + off) * Wx + iw + off) * Cinp + c] *
+                                 w[(size_t)o * Kd + (kh * KWp + kw) * Cinp + c];
+                acc += t;
+                sabs += fabs(t);
+              }
             }
+          for (int c = 0; c < ds_cin; ++c) {
+            const double t = (double)x2[(((size_t)n * H2 + 2 * oh) * W2 + 2 * ow) * ds_cin + c] * w[(size_t)o * Kd + K1 + c];
+            acc += t;
+            sabs += fabs(t);
+          }
           size_t oi = (((size_t)n * Ho + oh) * Wo + ow) * Cout + o;
-          if (res) acc += r[oi];
+          if (res) acc += r[oi], sabs += fabs(r[oi]);
           if (relu && acc < 0) acc = 0;
           double e = fabs(acc - y[oi]);
-          if (e > 1e-3 * (1 + fabs(acc))) { if (bad < 5) printf("  bad n%d oh%d ow%d o%d ref %f got %f\n", n, oh, ow, o, acc, y[oi]); ++bad; }
+          if (!(e <= tol * (1 + sabs))) { if (bad < 5) printf("  bad n%d oh%d ow%d o%d ref %f got %f\n", n, oh, ow, o, acc, y[oi]); ++bad; }
           maxerr = fmax(maxerr, e); maxref = fmax(maxref, fabs(acc));
         }
-  printf("%s N%d H%d W%d Cin%d Cout%d K%d s%d p%d res%d relu%d rc=%d maxerr %.3e (maxref %.3e) bad %ld\n",
-         bad ? "FAIL" : "ok  ", N, H, W, Cin, Cout, K, stride, pad, res, relu, rc, maxerr, maxref, bad);
+  printf("%s f32 N%d H%d W%d Cin%d Cout%d K%d s%d p%d res%d relu%d ds%d rc=%d maxerr %.3e (maxref %.3e) bad %ld\n",
+         bad || rc ? "FAIL" : "ok  ", N, H, W, Cin, Cout, K, stride, pad, res, relu, ds_cin, rc, maxerr, maxref, bad);
   hipFree(dx); hipFree(dw); hipFree(db); hipFree(dr); hipFree(dy);
-  return bad ? 1 : 0;
+  if (dx2) hipFree(dx2);
+  hipFree(dz);
+  return bad || rc ? 1 : 0;
 }
 
 static unsigned short f2bf(float f) {
@@ -430,6 +459,15 @@ int main() {
   fails += check(2, 30, 30, 3, 64, 7, 2, 3, true, false, true);
   fails += check(3, 37, 33, 3, 64, 7, 2, 3, true, false, true);  // odd sizes: row-width rounding, M tail
   fails += check(5, 1, 1, 512, 64, 1, 1, 0, false, false, false);
+  // f32 stride-1 3x3 convs at the stage shapes of R18/R50, the fused downsample (K columns
+  // [K1, K) from x2), ragged maps and M tails; exact-f32 products, so a tight bound
+  fails += check(12, 56, 56, 64, 64, 3, 1, 1, false, true, true, 0, 2e-6);
+  fails += check(5, 28, 28, 128, 128, 3, 1, 1, false, false, true, 64, 2e-6);
+  fails += check(6, 14, 14, 256, 256, 3, 1, 1, false, true, true, 0, 2e-6);
+  fails += check(4, 14, 14, 256, 256, 3, 1, 1, false, false, true, 128, 2e-6);
+  fails += check(3, 7, 7, 512, 512, 3, 1, 1, false, false, true, 256, 2e-6);
+  fails += check(3, 9, 11, 32, 64, 3, 1, 1, false, true, false, 0, 2e-6);
+  fails += check(2, 5, 3, 48, 128, 3, 1, 1, false, true, true, 0, 2e-6);
   printf("%d failures\n", fails);
   return fails;
 }

@@ -51,13 +51,28 @@ def config3(args):
     plans = [tn.myEpisodeDataloader.get_episode_plan() for _ in range(args.episodes)]
     B = args.batch
     tn._aug_batch(plans[:B], gal)  # warmup
+    bb = tn.mymodel.native(224, 224)
     torch.cuda.synchronize()
+    bb.profile(True)
     t0 = time.perf_counter()
     preds = []
     for b0 in range(0, len(plans), B):
         preds += tn._aug_batch(plans[b0:b0 + B], gal)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    ms, fl, nl = bb.profile_read()
+    bb.profile(False)
+    conv_ms = float(ms.sum())
+    peak = {"f32": 157.3, "bf16": 2516.6, "f32x3": round(2516.6 / 3, 1)}[args.dtype]
+    achieved = float(fl.sum()) / (conv_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": f"conv family: {int(nl.sum())} conv launches of the timed region, summed algorithmic "
+                          "FLOPs / summed HIP-event durations",
+                "conv_share_of_wall": round(conv_ms * 1e-3 / el, 3)}
+    cpu = None
+    if args.cpu_episodes:
+        cpu = c3_cpu_baseline(tn, gal, plans[:args.cpu_episodes], preds[:args.cpu_episodes])
     acc = float(np.mean([p == q["query_y"] for p, q in zip(preds, plans)]))
     reforward = os.environ.get("EOSV_AUG_REFORWARD", "0") == "1"
     # backbone frames per episode: query (<=16) + 5 supports x 16 (+ 40 augmented clips x 16 when
@@ -70,7 +85,57 @@ def config3(args):
             "clips_per_s": round(args.episodes * 46 / el, 1),
             "backbone_frames_per_episode": frames_ep, "backbone_frames_per_s": round(args.episodes * frames_ep / el, 1),
             "end_to_end_tflops": round(args.episodes * frames_ep * gflop / el / 1e3, 1),
-            "gallery_s": round(t_gal, 3), "gallery_frames": 10240, "episode_acc": acc}
+            "gallery_s": round(t_gal, 3), "gallery_frames": 10240, "episode_acc": acc,
+            "roofline": roofline, "cpu_baseline": cpu}
+
+
+def c3_cpu_baseline(tn, gal, plans, gpu_preds):
+    """The oracle's aug_seg_T episode (oracle/harness_ref.aug_segment_episode, torch-CPU fp32
+    restatement of network_test.py:195-259) on the box's host cores, per episode, with the gallery
+    segment features handed over from the GPU run (the gallery is built once per run, outside the
+    per-episode loop, on both sides) and gallery frames generated on demand.  Also reports whether
+    the oracle's predictions equal the GPU leg's on those episodes."""
+    sys.path.insert(0, REPO)
+    import numpy as np
+    import torch
+
+    import generate_augmented_datasets as gad
+    from eosv import arch, synth
+    from oracle import harness_ref, resnet_ref
+
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", 10 ** 6)))
+    torch.set_num_threads(threads)
+    model = resnet_ref.build_model("resnet50", {k: v.detach().cpu().numpy() for k, v in tn.mymodel.state_dict().items()})
+    infos = gad.gallery_video_infos()
+
+    class GallerySegments:  # [G, seg_len, 3, H, W], generated when indexed
+        def __getitem__(self, g):
+            vi = infos[(2 * g) // 16 % len(infos)]
+            ids, _ = synth.clip_frame_ids(vi, 16)
+            f0 = (2 * g) % 16
+            return torch.from_numpy(synth.synth_video(vi.split("/")[0], vi, ids[f0:f0 + 2], 224, 224))
+
+    def load(vi, support):
+        ids, n_all = synth.clip_frame_ids(vi, 16)
+        v = torch.from_numpy(synth.synth_video(vi.split("/")[0], vi, ids, 224, 224))
+        if support and v.shape[0] < 16:
+            v = torch.cat([v, torch.zeros(16 - v.shape[0], 3, 224, 224)])
+        return v, v.shape[0]
+
+    g = gal.cpu().numpy()
+    t = 0.0
+    equal = 0
+    for p, gp in zip(plans, gpu_preds):
+        t0 = time.perf_counter()
+        r = harness_ref.aug_segment_episode(model, p, load, g, GallerySegments(), len(set(p["support_y"])),
+                                            len(p["support"]) // len(set(p["support_y"])))
+        t += time.perf_counter() - t0
+        equal += int(int(r["pred"][0]) == int(gp))
+    n = len(plans)
+    return {"value": round(n / t, 4), "unit": "episodes/s", "cores": threads, "kind": "port",
+            "sample": f"{n} aug_seg_T episodes through oracle/harness_ref.aug_segment_episode (R50 fp32 torch-CPU, "
+                      f"gallery features from the GPU run, frame synthesis included); {t:.1f}s",
+            "pred_equal_vs_gpu_leg": f"{equal}/{n}"}
 
 
 def main():
@@ -80,6 +145,7 @@ def main():
     ap.add_argument("--episodes", type=int, default=64)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-episodes", type=int, default=0, help="config 3: oracle episodes for cpu_baseline")
     ap.add_argument("--max-frames", type=int, default=2048, help="backbone chunk (configs 4 / 5)")
     args = ap.parse_args()
     if args.config == 3:
