@@ -61,11 +61,25 @@ struct ConvArgs {
   // (oh, ow) -> x2 pixel (oh * stride2, ow * stride2), channel k - K1; nullptr = none
   const void* x2;     // NHWC [N, H2, W2, Cin2]
   int H2, W2, Cin2, stride2, K1;
-  // bf16 kernels, EOSV_F32X3: activations are [pixel][3 * C] bf16 = (hi, lo, hi) blocks of C
-  // channels; Cin / Cin2 / K count those 3C virtual input channels (weights (w_hi, w_hi, w_lo)),
-  // Cout is the logical C.  The epilogue reads the residual as hi + lo and stores hi, lo, hi.
+  // bf16 kernels, EOSV_F32X3: activations are stored [pixel][2 * C] bf16 = (hi, lo) blocks of C
+  // channels and read as 3C virtual input channels (hi, lo, hi): Cin / Cin2 / K count those
+  // (weights (w_hi, w_hi, w_lo)), virtual channel c >= 2C is physical channel c - 2C
+  // (split_chan), Cout is the logical C.  The epilogue reads the residual as hi + lo and stores
+  // hi, lo.
   int split;
+  // physical pixel strides (elements) of x and x2: Cin / Cin2, or 2/3 of them when split
+  // (0 = derive; conv_pixel_strides)
+  int xs, x2s;
 };
+
+__host__ __device__ inline int split_chan(int c, int cin3) {
+  const int c2 = 2 * (cin3 / 3);
+  return c >= c2 ? c - c2 : c;
+}
+inline void conv_pixel_strides(ConvArgs& a) {
+  if (!a.xs) a.xs = a.split ? 2 * (a.Cin / 3) : a.Cin;
+  if (!a.x2s) a.x2s = a.split ? 2 * (a.Cin2 / 3) : a.Cin2;
+}
 
 // Workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one L2;
 // MI355X_MICROARCH.md, Workgroup dispatch).  Remap so that XCD x processes the contiguous

@@ -29,7 +29,8 @@ __device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__
 
 // MF = MFMA tile edge: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16; same
 // cycles per FLOP, but the chip holds a higher clock on it with random operands)
-// SPLIT: EOSV_F32X3 epilogue (ConvArgs::split): residual = hi + lo, output stored as (hi, lo, hi)
+// SPLIT: EOSV_F32X3 (ConvArgs::split): A reads virtual channel blocks (hi, lo, hi) of the stored
+// (hi, lo) pixels; epilogue residual = hi + lo, output stored as (hi, lo)
 template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BK = 64;  // bf16 elements per row = 128 B
@@ -83,10 +84,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         // padded coordinates of tap (0, 0) are (oh*stride, ow*stride)
         arow[j] = x + ((long long)img * (a.H + 2 * a.pad) + oh * a.stride) * xrow + (long long)ow * a.stride * 3;
       } else {
-        arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 8;
+        arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.xs + lc * 8;
         if constexpr (DS)
           arow2[j] = (const u16*)a.x2 +
-                     (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 + lc * 8;
+                     (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.x2s + lc * 8;
       }
     } else {
       aih[j] = -(1 << 28);
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     } else if (DS && k0 >= a.K1) {
 #pragma unroll
       for (int j = 0; j < (DS ? AI : 1); ++j) {
-        const u16* src = arow2[j] ? arow2[j] + (k0 - a.K1) : zero;
+        const u16* src = arow2[j] ? arow2[j] + (SPLIT ? split_chan(k0 - a.K1, a.Cin2) : k0 - a.K1) : zero;
         u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
       }
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
-      const long long toff = ((long long)kh * a.W + kw) * a.Cin + c0;
+      const long long toff = ((long long)kh * a.W + kw) * a.xs + (SPLIT ? split_chan(c0, a.Cin) : c0);
 #pragma unroll
       for (int j = 0; j < AI; ++j) {
         const int ih = aih[j] + kh, iw = aiw[j] + kw;
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int NPASS = BM / WM / 32;
   constexpr int IPT = EPR * (BN / 8) / (64 * NW);   // 16-B output chunks per thread per pass
   static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
-  const long long ostr = SPLIT ? 3LL * a.Cout : a.Cout;  // output / residual pixel stride
+  const long long ostr = SPLIT ? 2LL * a.Cout : a.Cout;  // output / residual pixel stride
   const long long tile_bytes = (long long)min(BM, M - m0) * ostr * 2;
   const int nrec = (int)min(tile_bytes, 0x7fffffffLL);
   const __amdgpu_buffer_rsrc_t yr =
@@ -351,10 +352,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
           pl[k] = (unsigned)f_to_bf(lo - bf_to_f(blo)) | ((unsigned)f_to_bf(hi - bf_to_f(bhi)) << 16);
       }
       __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff, 0, 0);
-      if constexpr (SPLIT) {
-        __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff + 4 * a.Cout, 0, 0);
-      }
+      if constexpr (SPLIT) __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
     }
   }
 }
@@ -394,6 +392,7 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   static const int abl = env_switch("EOSV_CONV_ABL", 0);  // profiling-only ablations; results are wrong when set
   ConvArgs a = a0;
   a.abl = abl;
+  conv_pixel_strides(a);
   const bool stem = (a.Cin == 3);
   if (!a.zero || a.K % 64 != 0 || (!stem && a.Cin % 64 != 0) ||
       (stem && (a.KWp != 8 || a.KW != 7 || a.stride % 2 != 0 || a.K != (a.KH * 24 + 63) / 64 * 64))) {

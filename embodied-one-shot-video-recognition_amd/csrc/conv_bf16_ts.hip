@@ -81,7 +81,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
     if (piece < AP && row <= BM + 1 && p >= 0 && p < M) {
       const int rem = p % HW;
       const int oh = rem / a.W;
-      apix[t] = x + (long long)p * a.Cin + (sl ^ ((row >> 1) & 3)) * 8;
+      apix[t] = x + (long long)p * a.xs + (sl ^ ((row >> 1) & 3)) * 8;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh)
         if ((unsigned)(oh + kh - 1) < (unsigned)a.H) amask[t] |= 1u << kh;
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
     if (x2 && piece < AP && row >= 1 && row <= BM && p < M) {
       const int img = p / HW, rem = p - img * HW;
       const int oh = rem / a.W, ow = rem - oh * a.W;
-      apix2[t] = x2 + (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 +
+      apix2[t] = x2 + (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.x2s +
                  (sl ^ ((row >> 1) & 3)) * 8;
     }
   }
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
     btap[t] = kw;
     bsrc[t] = w + (long long)(n0 + row - kw * BN) * a.K + (sl ^ ((row >> 1) & 3)) * 8;
   }
-  const long long rowoff = (long long)a.W * a.Cin;  // elements from input row oh to oh + 1
+  const long long rowoff = (long long)a.W * a.xs;  // elements from input row oh to oh + 1
   auto kidx = [&](int kh, int kw, int c) -> int {   // K column of tap (kh, kw), channel c (32-aligned)
     return a.kcm ? (((c >> 6) * 9 + kh * 3 + kw) << 6) + (c & 63) : (kh * 3 + kw) * a.Cin + c;
   };
@@ -127,7 +127,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
 #pragma unroll
       for (int t = 0; t < APW; ++t) {
         const int piece = wid + NW * t;
-        if (piece < AP) dma16(apix2[t] + (apix2[t] != zero ? c0 : 0), As + piece * 16 * BK);
+        if (piece < AP)
+          dma16(apix2[t] + (apix2[t] != zero ? (SPLIT ? split_chan(c0, a.Cin2) : c0) : 0), As + piece * 16 * BK);
       }
 #pragma unroll
       for (int t = 0; t < BPW; ++t)
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
       return;
     }
     const int cs = st / 3, kh = st - 3 * cs, c0 = cs * BK;
-    const long long aoff = (long long)(kh - 1) * rowoff + c0;
+    const long long aoff = (long long)(kh - 1) * rowoff + (SPLIT ? split_chan(c0, a.Cin) : c0);
 #pragma unroll
     for (int t = 0; t < APW; ++t) {
       const int piece = wid + NW * t;
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   constexpr int NPASS = BM / WM / 32;
   constexpr int IPT = EPR * (BN / 8) / (64 * NW);
   static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
-  const long long ostr = SPLIT ? 3LL * a.Cout : a.Cout;
+  const long long ostr = SPLIT ? 2LL * a.Cout : a.Cout;
   const long long tile_bytes = (long long)min(BM, M - m0) * ostr * 2;
   const int nrec = (int)min(tile_bytes, 0x7fffffffLL);
   const __amdgpu_buffer_rsrc_t yr =
@@ -299,10 +300,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
           pl[k] = (unsigned)f2bf(lo - bf2f(blo)) | ((unsigned)f2bf(hi - bf2f(bhi)) << 16);
       }
       __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff, 0, 0);
-      if constexpr (SPLIT) {
-        __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff + 4 * a.Cout, 0, 0);
-      }
+      if constexpr (SPLIT) __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
     }
   }
 }

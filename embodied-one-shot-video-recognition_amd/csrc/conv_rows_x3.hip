@@ -1,9 +1,9 @@
 // Row-strip direct 3x3 conv for ResNet stage 1 in the f32x3 (split-bf16) mode: 64 -> 64
 // channels, stride 1, pad 1, 56-wide maps (R18 layer1, R50 layer1 c2 at 224x224).
 //
-// f32x3 activations are [pixel][192] bf16 = (hi, lo, hi) blocks of 64 channels and a conv sums
-// hi.w_hi + lo.w_hi + hi.w_lo (ConvArgs::split).  On the implicit GEMM that is K = 1728 with
-// the hi block staged twice; stage 1 (Cout 64) ran there at ~29 % of the bf16 MFMA rate and was
+// f32x3 activations are stored [pixel][128] bf16 = (hi, lo) blocks of 64 channels and a conv
+// sums hi.w_hi + lo.w_hi + hi.w_lo (ConvArgs::split).  On the implicit GEMM that is K = 1728
+// over the virtual (hi, lo, hi) channels, the hi block staged twice; stage 1 (Cout 64) ran there at ~29 % of the bf16 MFMA rate and was
 // a third of the f32x3 forward.  Here, as in conv_rows_bf16.hip, a persistent workgroup per CU
 // streams input strips through LDS and reads the A fragments straight from the staged rows,
 // but the weights (w_hi and w_lo: 2 x 72 KiB) cannot share the LDS with the strips, so they
@@ -11,12 +11,11 @@
 //  * 4 waves, wave g computes couts 16g .. 16g+15 of every pixel of the strip; its 36 weight
 //    fragments (w_hi and w_lo, 18 k-steps of 32) are loaded once per kernel;
 //  * a strip is TR = 2 output rows (112 pixels = 7 tiles of 16); LDS holds its 4 padded input
-//    rows as two planes (hi, lo) of [4 rows][58 slots][64 ch], double-buffered (120 KiB); the
-//    duplicate hi block is never read;
+//    rows as two planes (hi, lo) of [4 rows][58 slots][64 ch], double-buffered (120 KiB);
 //  * per k-step a wave reads 14 pixel fragments (hi and lo of 7 tiles) and issues 21 MFMAs
 //    (w_hi.hi, w_lo.hi, w_hi.lo per tile): 0.67 KiB of LDS reads per MFMA;
 //  * epilogue from registers: acc + shift + (res_hi + res_lo), ReLU, split into
-//    hi = bf16(v), lo = bf16(v - hi), stored as (hi, lo, hi) -- the same arithmetic as the
+//    hi = bf16(v), lo = bf16(v - hi), stored as (hi, lo) -- the same arithmetic as the
 //    implicit GEMM's split epilogue (conv_bf16.hip).
 // Same staged layout and swizzle as conv_rows_bf16.hip (16-B chunk c of slot p at c ^ (p & 7));
 // strips are dealt XCD-contiguously so that neighbouring strips (which share 2 input rows)
@@ -46,7 +45,8 @@ constexpr int PPW = PIECES / NW;
 constexpr int BUF = PIECES * 512;                              // bf16 elements per buffer (60 KiB)
 constexpr int TILES = TR * RW / 16;                            // 7
 constexpr int C = 64;                                          // logical channels
-constexpr int PIX = 3 * C;                                     // split pixel stride (hi, lo, hi)
+constexpr int PIX = 2 * C;                                     // stored split pixel stride (hi, lo)
+constexpr int VC = 3 * C;                                      // virtual input channels (hi, lo, hi)
 static_assert(TR * RW == TILES * 16, "strip = 7 pixel tiles");
 static_assert(2 * PLANE_PIECES <= PIECES && PIECES % NW == 0, "DMA pieces");
 static_assert(2 * BUF * 2 <= 163840, "LDS budget");
@@ -84,8 +84,8 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
 #pragma unroll
     for (int t = 0; t < 18; ++t) {
       const int tap = t >> 1, c = (4 * (t & 1) + q) * 8;
-      const int khi = a.kcm ? tap * 64 + c : tap * PIX + c;
-      const int klo = a.kcm ? (18 + tap) * 64 + c : tap * PIX + 2 * C + c;
+      const int khi = a.kcm ? tap * 64 + c : tap * VC + c;
+      const int klo = a.kcm ? (18 + tap) * 64 + c : tap * VC + 2 * C + c;
       whi[t] = *(const bf16x8*)(wr + khi);
       wlo[t] = *(const bf16x8*)(wr + klo);
     }
@@ -230,12 +230,11 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
       if (abl & 64) continue;
       asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(hv) : "memory");
       asm volatile("global_store_dwordx2 %0, %1, off offset:128" ::"v"(dst), "v"(lv) : "memory");
-      asm volatile("global_store_dwordx2 %0, %1, off offset:256" ::"v"(dst), "v"(hv) : "memory");
     }
-    // the next strip's DMA (issued before this strip's 21 stores) has landed, and every wave's
+    // the next strip's DMA (issued before this strip's 14 stores) has landed, and every wave's
     // reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
     if (abl & 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
   }
@@ -243,8 +242,8 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
 }
 
 bool conv_rows_x3_ok(const ConvArgs& a) {
-  return a.split && a.Cin == PIX && a.Cout == C && a.KH == 3 && a.KW == 3 && a.KWp == 3 && a.stride == 1 &&
-         a.pad == 1 && a.W == RW && a.H % TR == 0 && a.Ho == a.H && a.Wo == a.W && a.K == 9 * PIX && !a.x2 &&
+  return a.split && a.Cin == VC && a.xs == PIX && a.Cout == C && a.KH == 3 && a.KW == 3 && a.KWp == 3 && a.stride == 1 &&
+         a.pad == 1 && a.W == RW && a.H % TR == 0 && a.Ho == a.H && a.Wo == a.W && a.K == 9 * VC && !a.x2 &&
          a.zero;
 }
 

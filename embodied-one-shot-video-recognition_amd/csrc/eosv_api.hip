@@ -90,8 +90,8 @@ static int conv_out(int h, int k, int s, int p) { return (h + 2 * p - k) / s + 1
 static bool x3(const eosv_handle* h) { return h->d.dtype == EOSV_F32X3; }
 static bool conv_bf(const eosv_handle* h) { return h->d.dtype != EOSV_F32; }
 static bool stem_bf(const eosv_handle* h) { return h->d.dtype == EOSV_BF16; }
-// bytes per activation element: f32 4, bf16 2, split (hi, lo, hi) 6
-static size_t act_bytes(const eosv_handle* h) { return x3(h) ? 6 : conv_bf(h) ? 2 : 4; }
+// bytes per activation element: f32 4, bf16 2, split (hi, lo) 4
+static size_t act_bytes(const eosv_handle* h) { return x3(h) ? 4 : conv_bf(h) ? 2 : 4; }
 
 static Conv make_conv(int cin, int cout, int k, int stride, int pad, const std::string& wname,
                       const std::string& bnname) {
@@ -204,7 +204,8 @@ static int build_plan(eosv_handle* h) {
   h->fc.id = id++;
   h->n_layers = id;
   if (x3(h)) {
-    // split layout: every block conv reads 3 * cin virtual channels (hi, lo, hi)
+    // split layout: every block conv reads 3 * cin virtual channels (hi, lo, hi) of the stored
+    // (hi, lo) pixels
     auto widen = [](Conv& c) {
       c.cinp = 3 * c.cin;
       c.K = c.kh * c.kw * c.cinp;
@@ -408,6 +409,8 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   a.xcd = xcd;
   a.kcm = c.kcm ? 1 : 0;
   a.split = (bf16 && x3(h)) ? 1 : 0;
+  a.xs = a.split ? 2 * c.cin : c.cinp;  // physical pixel strides (the split layout stores hi, lo)
+  a.x2s = x2 ? (a.split ? 2 * (c.kds / 3) : c.kds) : 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);

@@ -146,8 +146,8 @@ __global__ void avgpool_kernel(const void* __restrict__ xv, int B, int HW, int C
   float s = 0.f;
   if constexpr (SPLIT) {
     // EOSV_F32X3 layout [pixel][hi C | lo C | hi C]: value = hi + lo (exact in f32)
-    const unsigned short* x = (const unsigned short*)xv + b * HW * 3 * C + c;
-    for (int p = 0; p < HW; ++p) s += bf2f(x[(long long)p * 3 * C]) + bf2f(x[(long long)p * 3 * C + C]);
+    const unsigned short* x = (const unsigned short*)xv + b * HW * 2 * C + c;
+    for (int p = 0; p < HW; ++p) s += bf2f(x[(long long)p * 2 * C]) + bf2f(x[(long long)p * 2 * C + C]);
   } else if constexpr (BF16) {
     const unsigned short* x = (const unsigned short*)xv + b * HW * C + c;
     for (int p = 0; p < HW; ++p) s += bf2f(x[(long long)p * C]);

@@ -512,7 +512,7 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
 // w_hi.x_hi + w_hi.x_lo + w_lo.x_hi in f32 (the x_lo.w_lo term, ~2^-16 relative, is dropped, as
 // in the split convs; tests/test_gpu_parity.py bounds the features at 1e-4 of the f32 oracle).
 // Replaces the exact-f32 MFMA stem (v_mfma_f32_16x16x4_f32: 16x fewer FLOP/clk than bf16).
-// Output: pooled map in the split layout [pixel][hi 64 | lo 64 | hi 64].
+// Output: pooled map in the split layout [pixel][hi 64 | lo 64].
 // LDS (56 KiB -> 2 workgroups per CU): w_lo [64][192] (16-B chunk c of row r at
 // (c & ~7) | ((c ^ (r >> 1)) & 7): conflict-free A-fragment reads); x_hi and x_lo rings, ONE copy
 // each (16 rows x 736 B), read as 4 dwords per B fragment (4-B aligned sources: no shifted
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_x3_cb_kernel(const
   f32x4 prev[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
-  u16* yimg = y + (long long)img * Hq * Wq * 192;
+  u16* yimg = y + (long long)img * Hq * Wq * 128;
   const int px = 7 * (t0 + wid) + (r16 >> 1);
   const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
   const bool dtask = tid < 4 * CB_GP;
@@ -703,12 +703,11 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_x3_cb_kernel(const
       }
     }
     if (writer) {
-      u16* o = yimg + ((long long)py * Wq + px) * 192 + 4 * q;
+      u16* o = yimg + ((long long)py * Wq + px) * 128 + 4 * q;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         *(uint2*)(o + j * 16) = ph[j];
         *(uint2*)(o + 64 + j * 16) = pl[j];
-        *(uint2*)(o + 128 + j * 16) = ph[j];
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -723,7 +722,7 @@ bool stem_pool_x3_ok(int H, int W) {
 }
 
 // w: [hi 64 x 192 | lo 64 x 192] bf16 (stem K layout [kh 8][24]), bias f32 [64], frames f32 NCHW,
-// y: split layout [N][Hq][Wq][192]
+// y: split layout [N][Hq][Wq][128] (hi 64 | lo 64)
 int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w, const float* bias, void* y,
                         hipStream_t s) {
   if (!stem_pool_x3_ok(H, W)) return set_error("stem_pool_x3: unsupported frame shape"), EOSV_ERR_UNSUPPORTED;

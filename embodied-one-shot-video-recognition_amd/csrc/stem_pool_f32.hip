@@ -58,7 +58,7 @@ __device__ __forceinline__ float row_shl(float v, int sh) {
 
 // x: padded f32 RGB [N][H+6][Wp][3] (stem_row_pixels), w: [64][176] f32, bias [64] f32,
 // y: [N][Hq][Wq][64] f32 (pooled).  Grid = N images, block = 64 * ntiles threads.
-// SPLIT (EOSV_F32X3): y is [N][Hq][Wq][192] bf16, (hi, lo, hi) of each pooled f32 value.
+// SPLIT (EOSV_F32X3): y is [N][Hq][Wq][128] bf16, (hi, lo) of each pooled f32 value.
 template <bool SPLIT>
 __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                              const float* __restrict__ w,
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
 #pragma unroll
   for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
   float* yimg = (float*)y + (long long)img * Hq * Wq * 64;
-  unsigned short* ysp = (unsigned short*)y + (long long)img * Hq * Wq * 192;
+  unsigned short* ysp = (unsigned short*)y + (long long)img * Hq * Wq * 128;
   const int px = 7 * wid + (r16 >> 1);  // pooled column this lane writes (even r16 <= 12)
   const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
 
@@ -181,10 +181,9 @@ __global__ __launch_bounds__(64 * SPF_MAX_TILES, 2) void stem_pool_f32_kernel(co
           lo[h] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(r0)) |
                   ((unsigned)__bfloat16_as_ushort(__float2bfloat16(r1)) << 16);
         }
-        unsigned short* d = ysp + ((long long)py * Wq + px) * 192 + j * 16 + 4 * q;
+        unsigned short* d = ysp + ((long long)py * Wq + px) * 128 + j * 16 + 4 * q;
         *(uint2*)d = make_uint2(hi[0], hi[1]);
         *(uint2*)(d + 64) = make_uint2(lo[0], lo[1]);
-        *(uint2*)(d + 128) = make_uint2(hi[0], hi[1]);
       } else {
         *(float4*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
       }

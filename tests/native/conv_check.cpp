@@ -294,7 +294,7 @@ static int check_stem_pool_x3(int N, int H, int W) {
   }
   float *dfr, *db;
   unsigned short *dw, *dy;
-  const size_t ny = (size_t)N * Hq * Wq * 192;
+  const size_t ny = (size_t)N * Hq * Wq * 128;  // split layout: (hi 64 | lo 64) per pixel
   hipMalloc(&dfr, fr.size() * 4); hipMalloc(&dw, w2.size() * 2); hipMalloc(&dy, ny * 2); hipMalloc(&db, 64 * 4);
   hipMemcpy(dfr, fr.data(), fr.size() * 4, hipMemcpyHostToDevice);
   hipMemcpy(dw, w2.data(), w2.size() * 2, hipMemcpyHostToDevice);
@@ -330,9 +330,10 @@ static int check_stem_pool_x3(int N, int H, int W) {
               const int sy = 2 * py + dy, sx = 2 * px + dx;
               if (sy >= 0 && sy < Hs && sx >= 0 && sx < Ws) m = fmax(m, st[((size_t)sy * Ws + sx) * 64 + o]);
             }
-          const size_t base = (((size_t)n * Hq + py) * Wq + px) * 192 + o;
+          const size_t base = (((size_t)n * Hq + py) * Wq + px) * 128 + o;
           const double got = (double)bf2f(y[base]) + bf2f(y[base + 64]);
-          const bool dup = y[base + 128] == y[base];
+          // lo is the rounding residual of hi: at most half an ulp of hi (2^-9 relative)
+          const bool dup = fabs(bf2f(y[base + 64])) <= fabs(bf2f(y[base])) * (1.0 / 256);
           const double e = fabs(got - m);
           maxref = fmax(maxref, fabs(m));
           if (e > 1e-4 * (1 + fabs(m)) || !dup) {
@@ -467,7 +468,7 @@ int main() {
   fails += check(4, 14, 14, 256, 256, 3, 1, 1, false, false, true, 128, 2e-6);
   fails += check(3, 7, 7, 512, 512, 3, 1, 1, false, false, true, 256, 2e-6);
   fails += check(3, 9, 11, 32, 64, 3, 1, 1, false, true, false, 0, 2e-6);
-  fails += check(2, 5, 3, 48, 128, 3, 1, 1, false, true, true, 0, 2e-6);
+  fails += check(2, 5, 3, 32, 128, 3, 1, 1, false, true, true, 32, 2e-6);
   printf("%d failures\n", fails);
   return fails;
 }

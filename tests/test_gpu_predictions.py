@@ -24,7 +24,10 @@ pytestmark = pytest.mark.gpu
 TAG = "c2_r18_preds1000_seed0"
 
 
-def test_thousand_reference_episodes_bit_exact(tmp_path, monkeypatch):
+@pytest.mark.parametrize("dtype", ["f32", "f32x3"])
+def test_thousand_reference_episodes_bit_exact(dtype, tmp_path, monkeypatch):
+    """f32 (exact-f32 MFMA) and f32x3 (split-bf16, f32-accurate): identical predictions on all
+    1000 reference episodes and embeddings within the 1e-4 bound."""
     import network_test
     import utils
 
@@ -38,6 +41,7 @@ def test_thousand_reference_episodes_bit_exact(tmp_path, monkeypatch):
     acc_path = str(tmp_path / "acc.txt")
     random.seed(meta["seed"])
     tn = network_test.TestNetwork(acc_path, "resnet18", "protonet", True)
+    tn.mymodel.compute_dtype = dtype
     tn.mymodel.max_frames = 2048
     tn.episodes_per_batch = 250
     tn.debug = {}
@@ -48,7 +52,7 @@ def test_thousand_reference_episodes_bit_exact(tmp_path, monkeypatch):
     ref_pred = arr["pred"]
     margin = arr["margin"]
     near = np.flatnonzero(margin < 1e-5)
-    print(f"[c2 x{n}] min top-2 margin {margin.min():.3e}, near ties (< 1e-5): {len(near)} {near.tolist()}")
+    print(f"[c2 x{n} {dtype}] min top-2 margin {margin.min():.3e}, near ties (< 1e-5): {len(near)} {near.tolist()}")
     assert np.array_equal(preds, ref_pred), np.flatnonzero(preds != ref_pred).tolist()
     text = open(acc_path).read()
     assert hashlib.sha256(text.encode()).hexdigest() == meta["acc_file_sha256"]
@@ -65,7 +69,7 @@ def test_thousand_reference_episodes_bit_exact(tmp_path, monkeypatch):
     got = np.concatenate([(sup @ r).reshape(n, n_sup), (q @ r)[:, None]], axis=1)
     bound = 1e-4 * np.sqrt(D) * max(np.abs(sup).max(), np.abs(q).max()) * np.linalg.norm(r)
     err = np.abs(got - arr["proj"]).max()
-    print(f"[c2 x{n}] max projection error {err:.3e} (bound {bound:.3e})")
+    print(f"[c2 x{n} {dtype}] max projection error {err:.3e} (bound {bound:.3e})")
     assert err <= bound
     assert len(plans["episodes"]) >= n
 
