@@ -41,6 +41,24 @@ constexpr int env_switch(const char*, int dflt) { return dflt; }
     }                                                                                      \
   } while (0)
 
+// ------------------------------------------------------------------ launch planning
+// A launcher given a LaunchInfo (ConvArgs::plan, or the stems' `info` argument) records its grid
+// instead of launching: the workgroups (persistent kernels: work items, e.g. row strips) and how
+// many of them the GPU runs at once.  The chunk planner (eosv_api.hip) prices a chunk size by
+// the wave quantisation this implies.
+struct LaunchInfo {
+  long long blocks;
+  long long slots;
+};
+int device_cu_count();  // CUs of the current device (cached; 256 on MI355X)
+// workgroups of `kernel` resident per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor), >= 1
+int kernel_occupancy(const void* kernel, int threads, size_t dyn_lds = 0);
+inline int record_launch(LaunchInfo* info, long long blocks, long long per_cu) {
+  info->blocks = blocks;
+  info->slots = per_cu * device_cu_count();
+  return EOSV_OK;
+}
+
 // ------------------------------------------------------------------ conv
 struct ConvArgs {
   const void* x;      // NHWC input [N,H,W,Cin]  (stem, Cin = 3: padded [N][H+2p][Wp][3])
@@ -70,6 +88,7 @@ struct ConvArgs {
   // physical pixel strides (elements) of x and x2: Cin / Cin2, or 2/3 of them when split
   // (0 = derive; conv_pixel_strides)
   int xs, x2s;
+  LaunchInfo* plan;   // host-side: non-null = record the grid (record_launch), launch nothing
 };
 
 __host__ __device__ inline int split_chan(int c, int cin3) {
@@ -98,13 +117,14 @@ bool conv_bf16_ts_ok(const ConvArgs& a);  // conv_bf16_ts.hip: tap-shift stride-
 int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s);
 bool stem_pool_bf16_ok(int H, int W, bool direct);  // stem_pool_bf16.hip: fused stem conv + ReLU + maxpool
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                          hipStream_t s, const float* frames = nullptr);
+                          hipStream_t s, const float* frames = nullptr, LaunchInfo* info = nullptr);
 bool stem_pool_x3_ok(int H, int W);  // stem_pool_bf16.hip: EOSV_F32X3 split-bf16 fused stem
 int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w, const float* bias, void* y,
-                        hipStream_t s);
+                        hipStream_t s, LaunchInfo* info = nullptr);
 bool stem_pool_f32_ok(int H, int W);  // stem_pool_f32.hip: the same for f32
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                         hipStream_t s, bool split = false);  // split: y in the EOSV_F32X3 (hi, lo, hi) layout
+                         hipStream_t s, bool split = false,  // split: y in the EOSV_F32X3 (hi, lo) layout
+                         LaunchInfo* info = nullptr);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv

@@ -367,6 +367,11 @@ static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
+  if (a.plan) {
+    static const int occ =
+        kernel_occupancy((const void*)conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false>, 64 * WM * WN);
+    return record_launch(a.plan, nb, occ);
+  }
   if (a.split) {
     if (STEM || (a.x2 && (a.K1 % 64 || a.Cin2 % 64)))
       return set_error("conv_bf16: split layout shape"), EOSV_ERR_UNSUPPORTED;

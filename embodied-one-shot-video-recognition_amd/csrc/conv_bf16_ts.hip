@@ -320,6 +320,11 @@ int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   const long long nb = ((M + BM - 1) / BM) * (a.Cout / BN);
   if (nb > 0x7fffffffLL) return set_error("conv_bf16_ts: grid too large"), EOSV_ERR_UNSUPPORTED;
 #define TS_LAUNCH(BM_, BN_, WM_, WN_)                                                                             \
+  if (a.plan) {                                                                                                  \
+    static const int occ = kernel_occupancy((const void*)conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, false>,           \
+                                            64 * WM_ * WN_);                                                     \
+    return record_launch(a.plan, nb, occ);                                                                       \
+  }                                                                                                              \
   if (a.split)                                                                                                   \
     hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, true>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), 0, \
                        s, a);                                                                                    \

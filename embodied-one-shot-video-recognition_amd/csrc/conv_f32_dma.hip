@@ -291,6 +291,11 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
+  if (a.plan) {
+    static const int occ = kernel_occupancy(
+        (const void*)conv_f32_dma_kernel<BM, BN, BK, WM, WN, false, NS, EPI, false>, 64 * WM * WN);
+    return record_launch(a.plan, nb, occ);
+  }
   if (a.x2) {
     if (STEM || a.K1 % BK || a.Cin2 % BK) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
     hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, false, NS, EPI, true>), dim3((unsigned)nb),

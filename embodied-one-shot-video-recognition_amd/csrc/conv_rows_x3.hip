@@ -259,6 +259,7 @@ int launch_conv_rows_x3(const ConvArgs& a, hipStream_t s) {
   if (nstrips <= 0) return EOSV_OK;
   if (nstrips > 0x7fffffffLL) return set_error("conv_rows_x3: too many strips"), EOSV_ERR_UNSUPPORTED;
   const unsigned grid = (unsigned)std::min<long long>(nstrips, ncu);
+  if (a.plan) return record_launch(a.plan, nstrips, 1);  // persistent: one workgroup per CU walks strips
 #ifdef EOSV_PROFILING
   if (a.abl)
     hipLaunchKernelGGL((conv_rows_x3_kernel<true, true>), dim3(grid), dim3(NT), 0, s, a, (int)nstrips);

@@ -22,6 +22,23 @@ namespace eosv {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+int device_cu_count() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) ||
+        c <= 0)
+      return 256;
+    return c;
+  }();
+  return n;
+}
+
+int kernel_occupancy(const void* kernel, int threads, size_t dyn_lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, dyn_lds) != hipSuccess || n < 1) n = 1;
+  return n;
+}
+
 #ifdef EOSV_PROFILING
 int env_switch(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -79,6 +96,11 @@ struct eosv_handle {
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   size_t pool_used = 0;
+  // chunk planner (eosv_backbone_forward): a dry run of forward_chunk prices a chunk size
+  bool planning = false;
+  double plan_cost = 0.0;
+  std::vector<double> chunk_cost;                          // by chunk size, filled on first use
+  std::unordered_map<int, std::vector<int>> chunk_plans;   // by frame count
 };
 
 namespace eosv {
@@ -373,6 +395,14 @@ static hipEvent_t prof_event(eosv_handle* h) {
   return h->pool[h->pool_used++];
 }
 
+// planning: a launch of `flops` algorithmic FLOPs on `li`'s grid costs flops / wave efficiency,
+// the efficiency being blocks / (slots x rounds): a grid of 4.67 waves runs 5
+static void add_plan_cost(eosv_handle* h, const LaunchInfo& li, double flops) {
+  if (li.blocks <= 0 || li.slots <= 0) return;
+  const double rounds = (double)((li.blocks + li.slots - 1) / li.slots);
+  h->plan_cost += flops * rounds * (double)li.slots / (double)li.blocks;
+}
+
 static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, int W, const void* res,
                     void* y, bool relu, bool bf16, hipStream_t s, const void* x2 = nullptr, int H2 = 0,
                     int W2 = 0, int stride2 = 1) {
@@ -411,6 +441,16 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   a.split = (bf16 && x3(h)) ? 1 : 0;
   a.xs = a.split ? 2 * c.cin : c.cinp;  // physical pixel strides (the split layout stores hi, lo)
   a.x2s = x2 ? (a.split ? 2 * (c.kds / 3) : c.kds) : 0;
+  // algorithmic FLOPs: logical channels (the split layout's 3x virtual K is not counted)
+  const double flops = 2.0 * N * a.Ho * a.Wo * c.cout *
+                       ((double)c.kh * c.kw * c.cin + (x2 ? c.kds / (a.split ? 3 : 1) : 0));
+  if (h->planning) {
+    LaunchInfo li{};
+    a.plan = &li;
+    const int prc = bf16 ? launch_conv_bf16(a, s) : launch_conv_f32(a, s);
+    if (prc == EOSV_OK) add_plan_cost(h, li, flops);
+    return prc;
+  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);
@@ -421,9 +461,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   const int rc = bf16 ? launch_conv_bf16(a, s) : launch_conv_f32(a, s);
   if (h->prof && rc == EOSV_OK) {
     EOSV_HIP_CHECK(hipEventRecord(e1, s));
-    // algorithmic MACs: logical channels (the split layout's 3x virtual K is not counted)
-    const double macs = (double)N * a.Ho * a.Wo * c.cout * ((double)c.kh * c.kw * c.cin + (x2 ? c.kds / (a.split ? 3 : 1) : 0));
-    h->recs.push_back({c.id, e0, e1, 2.0 * macs});
+    h->recs.push_back({c.id, e0, e1, flops});
   }
   return rc;
 }
@@ -488,8 +526,18 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
   if (x3(h) && !fused && !x3stem) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
   // the bf16 fused stem reads the f32 NCHW frames itself (no pack pass)
   const bool direct_bf = fused && sbf && direct;
-  if (!direct_bf && !x3stem && (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s))) return rc;
-  if (fused || x3stem) {
+  if (!direct_bf && !x3stem && !h->planning &&
+      (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s)))
+    return rc;
+  if (h->planning && (fused || x3stem)) {
+    LaunchInfo li{};
+    if ((rc = x3stem ? launch_stem_pool_x3(frames, B, H, W, h->stem_x3.w, h->stem_x3.b, bufs[1], s, &li)
+              : sbf  ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
+                                             direct_bf ? frames : nullptr, &li)
+                     : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s, x3(h), &li)))
+      return rc;
+    add_plan_cost(h, li, 2.0 * B * h->hs * h->ws * 64 * 147);
+  } else if (fused || x3stem) {
     // fused stem conv + ReLU + maxpool (profiled as the stem layer)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) {
@@ -509,7 +557,8 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
     }
   } else {
     if ((rc = run_conv(h, h->stem, h->pack, B, H, W, nullptr, bufs[0], true, bf, s))) return rc;
-    if ((rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s))) return rc;
+    if (!h->planning && (rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s)))
+      return rc;
   }
   int hh = h->hp, ww = h->wp;
   return run_blocks(h, 0, h->n_front, bufs[1], bufs, B, hh, ww, dst, xout, bf, s);
@@ -538,7 +587,62 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
   hh = h->front_hw[0];
   ww = h->front_hw[1];
   if ((rc = run_blocks(h, h->n_front, h->blocks.size(), x, h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
+  if (h->planning) return EOSV_OK;
   return launch_avgpool(x, B, hh * ww, h->D, feat, x3(h) ? 2 : bf ? 1 : 0, s);
+}
+
+// Chunk planner.  A launch's grid runs in whole waves of `slots` workgroups, so a chunk whose
+// grids end in a part-full wave pays for the empty slots (R18 layer 4 at 3122 frames: 1196
+// blocks of 256 x 256 = 4.67 waves of 256 -> 93 %).  The price of a chunk of F frames is the
+// dry-run forward's FLOPs divided by each launch's wave efficiency (add_plan_cost); B frames are
+// split into n - 1 chunks of c frames and a last one (n = the fewest chunks max_frames allows,
+// or one more), choosing c by that price.  Prices are computed once per handle for every chunk
+// size, plans once per frame count.  EOSV_CHUNK_PLAN=0 (profiling build): equal chunks.
+static double price_chunk(eosv_handle* h, int F) {
+  if (h->chunk_cost.empty()) {
+    h->chunk_cost.assign((size_t)h->d.max_frames + 1, 0.0);
+    for (int f = 1; f <= h->d.max_frames; ++f) {
+      h->planning = true;
+      h->plan_cost = 0.0;
+      // any non-null frame pointer: the launchers choose their kernel by it and record the grid
+      const int rc = forward_chunk(h, (const float*)h->zero, f, nullptr, nullptr);
+      h->planning = false;
+      h->chunk_cost[f] = rc ? 1e300 : h->plan_cost;
+    }
+  }
+  return h->chunk_cost[F];
+}
+
+static const std::vector<int>& plan_chunks(eosv_handle* h, int B) {
+  auto it = h->chunk_plans.find(B);
+  if (it != h->chunk_plans.end()) return it->second;
+  const int mf = h->d.max_frames;
+  const int nmin = (B + mf - 1) / mf;
+  std::vector<int> best;
+  {  // equal chunks (the plan before the planner)
+    const int csz = (B + nmin - 1) / nmin;
+    for (int b0 = 0; b0 < B; b0 += csz) best.push_back(std::min(csz, B - b0));
+  }
+  static const int on = env_switch("EOSV_CHUNK_PLAN", 1);
+  if (on) {
+    double bc = 0.0;
+    for (int nb : best) bc += price_chunk(h, nb);
+    for (int n = nmin; n <= nmin + 1; ++n) {
+      const int lo = (B + n - 1) / n;  // the largest chunk holds at least this
+      for (int c = lo; c <= std::min(mf, B); ++c) {
+        const int last = B - (n - 1) * c;
+        if (last <= 0) break;
+        if (last > c) continue;
+        const double cost = (n - 1) * price_chunk(h, c) + price_chunk(h, last);
+        if (cost < bc * (1.0 - 1e-9)) {
+          bc = cost;
+          best.assign((size_t)(n - 1), c);
+          best.push_back(last);
+        }
+      }
+    }
+  }
+  return h->chunk_plans.emplace(B, std::move(best)).first->second;
 }
 
 }  // namespace eosv
@@ -654,15 +758,12 @@ int eosv_backbone_forward(eosv_handle* h, const float* d_frames, int B, float* d
     return EOSV_ERR_STATE;
   }
   const size_t fstride = (size_t)3 * h->d.height * h->d.width;
-  // equal-size chunks (no small tail chunk): fewer, fuller launches
-  const int nchunks = (B + h->d.max_frames - 1) / h->d.max_frames;
-  const int csz = nchunks ? (B + nchunks - 1) / nchunks : 0;
-  for (int b0 = 0; b0 < B; b0 += csz) {
-    const int nb = std::min(csz, B - b0);
-
-    int rc = forward_chunk(h, d_frames + b0 * fstride, nb, d_feat + (size_t)b0 * h->D,
-                           (hipStream_t)stream);
+  if (B == 0) return EOSV_OK;
+  int b0 = 0;
+  for (const int nb : plan_chunks(h, B)) {
+    int rc = forward_chunk(h, d_frames + b0 * fstride, nb, d_feat + (size_t)b0 * h->D, (hipStream_t)stream);
     if (rc) return rc;
+    b0 += nb;
   }
   return EOSV_OK;
 }

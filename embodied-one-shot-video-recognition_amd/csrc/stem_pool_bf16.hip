@@ -724,12 +724,16 @@ bool stem_pool_x3_ok(int H, int W) {
 // w: [hi 64 x 192 | lo 64 x 192] bf16 (stem K layout [kh 8][24]), bias f32 [64], frames f32 NCHW,
 // y: split layout [N][Hq][Wq][128] (hi 64 | lo 64)
 int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w, const float* bias, void* y,
-                        hipStream_t s) {
+                        hipStream_t s, LaunchInfo* info) {
   if (!stem_pool_x3_ok(H, W)) return set_error("stem_pool_x3: unsupported frame shape"), EOSV_ERR_UNSUPPORTED;
   if (B <= 0) return EOSV_OK;
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int ncb = ((Wq + 6) / 7 + CB_TILES - 1) / CB_TILES;
+  if (info) {
+    static const int occ = kernel_occupancy((const void*)stem_pool_x3_cb_kernel, 64 * CB_TILES);
+    return record_launch(info, (long long)B * ncb, occ);
+  }
   hipLaunchKernelGGL(stem_pool_x3_cb_kernel, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w, bias,
                      (u16*)y, H, W, Hs, Ws, Hq, Wq);
   EOSV_LAUNCH_CHECK();
@@ -751,19 +755,24 @@ bool stem_pool_bf16_ok(int H, int W, bool direct) {
 
 // pack: padded bf16 RGB rows (pack_rgb_pad), or nullptr with `frames` = the f32 NCHW input
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                          hipStream_t s, const float* frames) {
+                          hipStream_t s, const float* frames, LaunchInfo* info) {
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int ntiles = (Wq + 6) / 7;
   if (frames && stem_cb() && W % 4 == 0 && Hs % 2 == 0) {
     if (B <= 0) return EOSV_OK;
     const int ncb = (ntiles + CB_TILES - 1) / CB_TILES;
+    if (info) {
+      static const int occ = kernel_occupancy((const void*)stem_pool_bf16_cb_kernel, 64 * CB_TILES);
+      return record_launch(info, (long long)B * ncb, occ);
+    }
     hipLaunchKernelGGL(stem_pool_bf16_cb_kernel, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w, bias,
                        (u16*)y, H, W, Hs, Ws, Hq, Wq);
     EOSV_LAUNCH_CHECK();
     return EOSV_OK;
   }
   if (ntiles > MAX_TILES || B <= 0) return B <= 0 ? EOSV_OK : (set_error("stem_pool: too wide"), EOSV_ERR_UNSUPPORTED);
+  if (info) return record_launch(info, B, 1);  // one image per workgroup, LDS-bound to 1 per CU
   const int Wp = stem_row_pixels(W, 3);
   if (frames) {
     if (4 * (Wp / 2) > 64 * ntiles) return set_error("stem_pool: direct rows need more threads"), EOSV_ERR_UNSUPPORTED;

@@ -203,7 +203,7 @@ bool stem_pool_f32_ok(int H, int W) {
 }
 
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                         hipStream_t s, bool split) {
+                         hipStream_t s, bool split, LaunchInfo* info) {
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int ntiles = (Wq + 6) / 7;
@@ -211,6 +211,10 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
   if (ntiles > SPF_MAX_TILES) return set_error("stem_pool_f32: too wide"), EOSV_ERR_UNSUPPORTED;
   const size_t lds = (size_t)(SPF_W_FLOATS + SPF_RING * spf_row_floats(stem_row_pixels(W, 3))) * 4;
   if (lds > 163840) return set_error("stem_pool_f32: rows too wide for LDS"), EOSV_ERR_UNSUPPORTED;
+  if (info) {
+    static const int occ = kernel_occupancy((const void*)stem_pool_f32_kernel<false>, 64 * ntiles, lds);
+    return record_launch(info, B, occ);
+  }
   if (split)
     hipLaunchKernelGGL(stem_pool_f32_kernel<true>, dim3(B), dim3(64 * ntiles), lds, s, (const float*)pack,
                        (const float*)w, bias, y, H, W, Hs, Ws, Hq, Wq);
