@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--seg-len", type=int, default=2)
     ap.add_argument("--max-frames", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--list", default=None,
+                    help="split list to sample episodes from (default: the reference's sources/data/test.list)")
     ap.add_argument("--cpu-baseline-sec", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
@@ -254,7 +256,8 @@ def main():
     T = args.segments * args.seg_len
     E = args.episodes_per_step
     n_steps = args.warmup + args.steps
-    plans = ep_mod.plan_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed)
+    lines = open(args.list).readlines() if args.list else None
+    plans = ep_mod.plan_episodes(E * n_steps * world, args.n_way, args.k_shot, "test", seed=args.seed, lines=lines)
     mine_idx = edist.shard_indices(len(plans), rank, world)  # episode e runs on rank e % world
     batches = []
     for s in range(n_steps):
@@ -309,7 +312,9 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic frames (deterministic, generated in HBM) + random-init weights of the "
-                    "reference architecture; episodes from the reference's test.list in its RNG order",
+                    "reference architecture; episodes from "
+                    + (os.path.relpath(args.list, REPO) if args.list else "the reference's test.list")
+                    + " in the reference's RNG order",
             "config": {"workload": f"test_network_baseline {args.n_way}-way {args.k_shot}-shot, "
                                    f"{args.segments} seg x {args.seg_len} frames, {args.arch}, "
                                    f"{args.res}x{args.res}, {args.dtype} ({args.config_label})",

@@ -151,7 +151,9 @@ def main():
     if args.config == 3:
         print(json.dumps(config3(args)), flush=True)
         return
-    shape = {4: ["--arch", "resnet50", "--n-way", "14", "--k-shot", "1", "--segments", "16"],
+    # config 4 samples the UnrealAction-shaped split (14 classes x 10 videos, tests/golden/unreal14.list)
+    shape = {4: ["--arch", "resnet50", "--n-way", "14", "--k-shot", "1", "--segments", "16",
+                 "--list", os.path.join(REPO, "tests", "golden", "unreal14.list")],
              5: ["--arch", "resnet101", "--n-way", "5", "--k-shot", "5", "--segments", "32", "--res", "256"]}[args.config]
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), *shape, "--dtype", args.dtype,
            "--episodes-per-step", str(args.episodes), "--steps", "2", "--no-cpu-baseline", "--secondary-dtype", "",
