@@ -156,7 +156,8 @@ def main():
                  "--list", os.path.join(REPO, "tests", "golden", "unreal14.list")],
              5: ["--arch", "resnet101", "--n-way", "5", "--k-shot", "5", "--segments", "32", "--res", "256"]}[args.config]
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), *shape, "--dtype", args.dtype,
-           "--episodes-per-step", str(args.episodes), "--steps", "2", "--no-cpu-baseline", "--secondary-dtype", "",
+           "--episodes-per-step", str(args.episodes), "--steps", "2", "--secondary-dtype", "",
+           "--cpu-baseline-sec", "10",
            "--max-frames", str(args.max_frames), "--config-label", f"BASELINE configs[{args.config - 1}]"]
     sys.exit(subprocess.call(cmd))
 
