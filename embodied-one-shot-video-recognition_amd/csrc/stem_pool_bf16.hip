@@ -418,14 +418,15 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int s = 0; s < 6; ++s) wf[j][s] = *(const bf16x8*)(w + (j * 16 + r16) * KSTEM + 32 * s + 8 * q);
-  f32x4 bv[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(bias + j * 16 + 4 * q);
-
   const int k = 14 * wid + r16;  // ring-relative stem column + 1
   const int m = k & 3;
   const int sx = 14 * (t0 + wid) - 1 + r16;
-  const float cmask = (sx >= 0 && sx < Ws) ? 0.f : -INFINITY;  // stem columns outside the map
+  // the accumulators start from the BN shift, or -inf for stem columns outside the map: such a
+  // column then pools as -inf with no per-step mask (the products are finite)
+  const float cmask = (sx >= 0 && sx < Ws) ? 0.f : -INFINITY;
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(bias + j * 16 + 4 * q) + cmask;
   const int xchunk = m * CB_CH + (12 * k + 4 * m) / 16;
 
   auto stem_row = [&](int sy, f32x4 (&acc)[4]) {
@@ -450,25 +451,23 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
   __syncthreads();
 
   const float NEG = -INFINITY;
-  f32x4 prev[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) prev[j] = f32x4{NEG, NEG, NEG, NEG};
   u16* yimg = y + (long long)img * Hq * Wq * 64;
   const int px = 7 * (t0 + wid) + (r16 >> 1);
   const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
   const bool dtask = tid < 4 * CB_GP;
   const int drow = tid / CB_GP, dg = tid - (tid / CB_GP) * CB_GP;
-  for (int py = 0; py < Hq; ++py) {
+  // one pooled row: stem rows 2py (into a1) and 2py + 1 (into a2), pooled with `prev` (stem row
+  // 2py - 1); the caller rotates the three arrays (no per-step copy of a2 into prev)
+  auto step = [&](int py, const f32x4 (&prev)[4], f32x4 (&a1)[4], f32x4 (&a2)[4]) {
     if (py + 1 < Hq) stage_f32(4 * py + 9);
-    f32x4 a1[4], a2[4];
     stem_row(2 * py, a1);
     stem_row(2 * py + 1, a2);
     // Pool on the accumulators, which start from the BN shift (max commutes with ReLU and the bf16
-    // rounding, both monotone).  VALU-lean: the SIMD's vector issue, not the MFMA pipe, bounded
-    // this loop (r01: ~290 VALU per wave-step against 48 MFMAs): Hs is even (launcher), so no stem
-    // row is past the map; the column mask is one add of 0 / -inf after the row max; the column
-    // max takes its neighbours by DPP (bound_ctrl: lanes past the 16-lane row read 0, they are
-    // not writers); the file is built with -fno-honor-nans (no canonicalising max per DPP value).
+    // rounding, both monotone) or -inf (columns outside the map).  VALU-lean: the SIMD's vector
+    // issue, not the MFMA pipe, bounded this loop (r01: ~290 VALU per wave-step against 48
+    // MFMAs): Hs is even (launcher), so no stem row is past the map; the column max takes its
+    // neighbours by DPP (bound_ctrl: lanes past the 16-lane row read 0, they are not writers);
+    // the file is built with -fno-honor-nans (no canonicalising max per DPP value).
     unsigned pk4[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -478,8 +477,7 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int e = 2 * e2 + h;
-          const float v = fmaxf(fmaxf(prev[j][e], a1[j][e]), a2[j][e]) + cmask;  // row max
-          prev[j][e] = a2[j][e];
+          const float v = fmaxf(fmaxf(prev[j][e], a1[j][e]), a2[j][e]);  // row max
           const float c = fmaxf(fmaxf(v, shl_dpp<1>(v)), shl_dpp<2>(v));
           o[h] = fmaxf(c, 0.f);  // the shift is in the accumulators
         }
@@ -501,7 +499,20 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
         *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk4[j][0], pk4[j][1]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  };
+  f32x4 ra[4], rb[4], rc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ra[j] = f32x4{NEG, NEG, NEG, NEG};
+  // rows rotate ra -> (rb, rc) -> (ra, rb) -> (rc, ra): three steps per iteration, each reading
+  // the previous step's second row as its `prev`
+  int py = 0;
+  for (; py + 3 <= Hq; py += 3) {
+    step(py, ra, rb, rc);
+    step(py + 1, rc, ra, rb);
+    step(py + 2, rb, rc, ra);
   }
+  if (py < Hq) step(py, ra, rb, rc);
+  if (py + 1 < Hq) step(py + 1, rc, ra, rb);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
