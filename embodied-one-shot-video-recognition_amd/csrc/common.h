@@ -142,5 +142,6 @@ int launch_maxpool3x3s2(const void* x, int B, int H, int W, int C, void* y, int 
                         int bf16, hipStream_t s);
 // bf16: 0 f32 input, 1 bf16, 2 the EOSV_F32X3 split layout (value = hi + lo)
 int launch_avgpool(const void* x, int B, int HW, int C, float* y, int bf16, hipStream_t s);
+int launch_act_to_f32(const void* x, long long n, int C, int mode, float* y, hipStream_t s);
 
 }  // namespace eosv

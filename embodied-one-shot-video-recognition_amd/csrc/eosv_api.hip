@@ -81,6 +81,8 @@ struct eosv_handle {
   void* sbuf[4] = {nullptr, nullptr, nullptr, nullptr};  // sub-chunk scratch for the front stages
   int sub_frames = 0;          // front-stage sub-chunk (0 = off)
   size_t n_front = 0;          // blocks in the front phase (layer1)
+  size_t stage_end[4] = {0, 0, 0, 0};  // blocks of layer1 .. layerN (cumulative)
+  int stage_hwc[5][3] = {};            // output (h, w, channels) of the stem + maxpool and each layer
   size_t front_out_elems = 0;  // per-frame elements of the layer1 output
   int front_hw[2] = {0, 0};
   std::vector<void*> allocs;
@@ -211,7 +213,14 @@ static int build_plan(eosv_handle* h) {
         h->front_hw[1] = ww;
       }
     }
+    h->stage_end[li] = h->blocks.size();
+    h->stage_hwc[li + 1][0] = hh;
+    h->stage_hwc[li + 1][1] = ww;
+    h->stage_hwc[li + 1][2] = inpl;
   }
+  h->stage_hwc[0][0] = h->hp;
+  h->stage_hwc[0][1] = h->wp;
+  h->stage_hwc[0][2] = 64;
   h->act_elems = act;
   Conv fc = make_conv(h->D, h->d.num_classes, 1, 1, 0, "fc.weight", "");
   h->fc = fc;
@@ -512,9 +521,8 @@ static bool stem_pool_fused(bool bf) {
   return bf ? vb : vf;
 }
 
-// stem -> maxpool -> stage-0 blocks for frames [0, B) of `frames`, output into `dst`
-static int run_front(eosv_handle* h, const float* frames, int B, void* const* bufs, void* dst, void** xout,
-                     bool bf, hipStream_t s) {
+// stem -> maxpool for frames [0, B) of `frames`, output into bufs[1]
+static int run_stem(eosv_handle* h, const float* frames, int B, void* const* bufs, bool bf, hipStream_t s) {
   const int H = h->d.height, W = h->d.width;
   int rc;
   static const bool direct = env_switch("EOSV_STEM_DIRECT", 1) != 0;  // 0 = pack kernel + LDS-DMA rows (A/B switch)
@@ -560,6 +568,14 @@ static int run_front(eosv_handle* h, const float* frames, int B, void* const* bu
     if (!h->planning && (rc = launch_maxpool3x3s2(bufs[0], B, h->hs, h->ws, 64, bufs[1], h->hp, h->wp, bf, s)))
       return rc;
   }
+  return EOSV_OK;
+}
+
+// stem -> maxpool -> stage-0 blocks for frames [0, B) of `frames`, output into `dst`
+static int run_front(eosv_handle* h, const float* frames, int B, void* const* bufs, void* dst, void** xout,
+                     bool bf, hipStream_t s) {
+  int rc;
+  if ((rc = run_stem(h, frames, B, bufs, bf, s))) return rc;
   int hh = h->hp, ww = h->wp;
   return run_blocks(h, 0, h->n_front, bufs[1], bufs, B, hh, ww, dst, xout, bf, s);
 }
@@ -766,6 +782,30 @@ int eosv_backbone_forward(eosv_handle* h, const float* d_frames, int B, float* d
     b0 += nb;
   }
   return EOSV_OK;
+}
+
+int eosv_backbone_probe(eosv_handle* h, const float* d_frames, int B, int stage, float* d_out,
+                        eosv_stream_t stream) {
+  if (!h || B < 1 || B > h->d.max_frames || stage < 0 || stage > 4 || !d_frames || !d_out) {
+    set_error("eosv_backbone_probe: bad argument (1 <= B <= max_frames, 0 <= stage <= 4)");
+    return EOSV_ERR_ARG;
+  }
+  if (!h->loaded) {
+    set_error("eosv_backbone_probe: weights not loaded");
+    return EOSV_ERR_STATE;
+  }
+  const bool bf = conv_bf(h);
+  const hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = run_stem(h, d_frames, B, h->buf, bf, s))) return rc;
+  void* x = h->buf[1];
+  int hh = h->hp, ww = h->wp;
+  if (stage > 0 && (rc = run_blocks(h, 0, h->stage_end[stage - 1], x, h->buf, B, hh, ww, nullptr, &x, bf, s)))
+    return rc;
+  const int* hwc = h->stage_hwc[stage];
+  const long long per_frame = (long long)hwc[0] * hwc[1] * hwc[2];
+  if ((rc = launch_act_to_f32(x, per_frame * B, hwc[2], x3(h) ? 2 : bf ? 1 : 0, d_out, s))) return rc;
+  return (int)per_frame;
 }
 
 int eosv_fc_forward(eosv_handle* h, const float* d_feat, int B, float* d_logits, eosv_stream_t stream) {

@@ -145,7 +145,7 @@ __global__ void avgpool_kernel(const void* __restrict__ xv, int B, int HW, int C
   const int c = (int)(t - b * C);
   float s = 0.f;
   if constexpr (SPLIT) {
-    // EOSV_F32X3 layout [pixel][hi C | lo C | hi C]: value = hi + lo (exact in f32)
+    // EOSV_F32X3 layout [pixel][hi C | lo C]: value = hi + lo (exact in f32)
     const unsigned short* x = (const unsigned short*)xv + b * HW * 2 * C + c;
     for (int p = 0; p < HW; ++p) s += bf2f(x[(long long)p * 2 * C]) + bf2f(x[(long long)p * 2 * C + C]);
   } else if constexpr (BF16) {
@@ -156,6 +156,29 @@ __global__ void avgpool_kernel(const void* __restrict__ xv, int B, int HW, int C
     for (int p = 0; p < HW; ++p) s += x[(long long)p * C];
   }
   y[t] = s / (float)HW;
+}
+
+// activation map -> f32, same NHWC order (eosv_backbone_probe); mode as launch_avgpool's bf16
+__global__ void act_to_f32_kernel(const void* __restrict__ xv, long long n, int C, int mode, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (mode == 2) {
+    const unsigned short* x = (const unsigned short*)xv;
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    y[i] = bf2f(x[p * 2 * C + c]) + bf2f(x[p * 2 * C + C + c]);
+  } else if (mode == 1) {
+    y[i] = bf2f(((const unsigned short*)xv)[i]);
+  } else {
+    y[i] = ((const float*)xv)[i];
+  }
+}
+
+int launch_act_to_f32(const void* x, long long n, int C, int mode, float* y, hipStream_t s) {
+  if (n <= 0) return EOSV_OK;
+  hipLaunchKernelGGL(act_to_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, C, mode, y);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
 }
 
 int launch_avgpool(const void* x, int B, int HW, int C, float* y, int bf16, hipStream_t s) {

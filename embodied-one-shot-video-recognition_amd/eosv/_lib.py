@@ -22,7 +22,7 @@ _STATUS = {-1: "EOSV_ERR_ARG", -2: "EOSV_ERR_HIP", -3: "EOSV_ERR_OOM",
            -4: "EOSV_ERR_UNSUPPORTED", -5: "EOSV_ERR_STATE"}
 
 # every symbol include/eosv.h declares
-EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_fc_forward",
+EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_backbone_probe", "eosv_fc_forward",
            "eosv_clip_embed", "eosv_segment_mean", "eosv_match", "eosv_segment_match", "eosv_segment_match_episodes",
            "eosv_temporal_smooth", "eosv_normalize_frames", "eosv_crop_normalize_frames", "eosv_synth_frames", "eosv_plan_episodes", "eosv_profile_enable", "eosv_profile_read", "eosv_feature_dim", "eosv_device_bytes", "eosv_last_error",
            "eosv_destroy")
@@ -55,6 +55,7 @@ def lib():
         "eosv_load_weights": (i32, [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
                                     ctypes.POINTER(i64), i32]),
         "eosv_backbone_forward": (i32, [vp, vp, i32, vp, vp]),
+        "eosv_backbone_probe": (i32, [vp, vp, i32, i32, vp, vp]),
         "eosv_fc_forward": (i32, [vp, vp, i32, vp, vp]),
         "eosv_clip_embed": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
         "eosv_segment_mean": (i32, [vp, i32, i32, i32, vp, vp]),

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import synth
-from ._lib import (EOSV_BF16, EOSV_F32, EOSV_F32X3, MATCH_COSINE, MATCH_PROTONET, MAX_COLS, EosvDesc, check,
+from ._lib import (EOSV_BF16, EOSV_F32, EOSV_F32X3, MATCH_COSINE, MATCH_PROTONET, MAX_COLS, EosvDesc, EosvError, check,
                    lib, ptr, stream_ptr)
 from .arch import SPECS
 
@@ -96,6 +96,33 @@ class Backbone:
             out = torch.empty(B, self.D, device=frames.device, dtype=torch.float32)
         check(lib().eosv_backbone_forward(self._h, ptr(frames), B, ptr(out), stream_ptr(stream)),
               "eosv_backbone_forward")
+        return out
+
+    def stage_shape(self, stage: int):
+        """(h, w, C) of the map after the stem + maxpool (stage 0) or after layer `stage`."""
+        out = lambda n, k, st, p: (n + 2 * p - k) // st + 1  # noqa: E731
+        h, w = out(out(self.height, 7, 2, 3), 3, 2, 1), out(out(self.width, 7, 2, 3), 3, 2, 1)
+        if stage == 0:
+            return h, w, 64
+        for _ in range(2, stage + 1):
+            h, w = out(h, 3, 2, 1), out(w, 3, 2, 1)
+        return h, w, (64 << (stage - 1)) * (4 if self.D == 2048 else 1)
+
+    def probe(self, frames: torch.Tensor, stage: int, stream=None) -> torch.Tensor:
+        """The map after the stem + maxpool (stage 0) or after layer `stage` (1..4), f32 NHWC
+        [B, h, w, C] (eosv_backbone_probe: diagnostics and the per-layer checksum test)."""
+        frames = frames.contiguous()
+        _require_cuda(frames, "frames", torch.float32)
+        if not 0 <= stage <= 4:
+            raise ValueError("stage must be 0..4")
+        B = frames.shape[0]
+        h, w, C = self.stage_shape(stage)
+        out = torch.empty(B, h, w, C, device=frames.device, dtype=torch.float32)
+        n = lib().eosv_backbone_probe(self._h, ptr(frames), B, int(stage), ptr(out), stream_ptr(stream))
+        if n < 0:
+            check(n, "eosv_backbone_probe")
+        if n != h * w * C:
+            raise EosvError(f"eosv_backbone_probe: {n} elements per frame, expected {h * w * C}")
         return out
 
     def fc(self, feat: torch.Tensor, stream=None) -> torch.Tensor:

@@ -169,6 +169,15 @@ int eosv_profile_read(eosv_handle* h, double* ms, double* flops, int64_t* launch
 int eosv_plan_episodes(const int32_t* class_sizes, int n_classes, int n_way, int k_shot, uint64_t seed,
                        int n_episodes, int32_t* classes, int32_t* query, int32_t* support);
 
+/* Diagnostics (SURVEY 8(c) one-frame per-layer checksums): the backbone on d_frames
+ * [B,3,H,W] (1 <= B <= max_frames) up to the end of `stage` -- 0 = stem + maxpool
+ * (convnet.0-3), 1..4 = layer1..layer4 (convnet.4-7) -- written to d_out as f32 NHWC
+ * [B, h, w, C] (converted from bf16 or the f32x3 split layout).  Returns the f32 elements per
+ * frame (h * w * C), or a negative eosv_status.  Replaces nothing on the reference's path: it
+ * exposes the intermediate maps of self.convnet (models.py:19) for parity checks. */
+int eosv_backbone_probe(eosv_handle* h, const float* d_frames, int B, int stage, float* d_out,
+                        eosv_stream_t stream);
+
 /* Feature dimension D of the handle's backbone. */
 int eosv_feature_dim(const eosv_handle* h);
 

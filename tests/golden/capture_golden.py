@@ -436,6 +436,37 @@ def pin_plans_to_fixture(meta, plans_tag="plans_test_seed0"):
     meta["n_episodes"] = len(eps)
 
 
+def capture_layer_checksums(mods, tag, archs=("resnet18", "resnet50")):
+    """one frame through the reference's model wrapper (models.py:9-37:
+    self.convnet = the torchvision children minus fc), checksums of the map after the stem +
+    maxpool (convnet.0-3) and after each of layer1..layer4 (convnet.4-7): sum, sum of squares,
+    max |.|, and the projection onto a fixed N(0,1) tensor of the map's NCHW shape
+    (numpy default_rng(1000 + stage)).  The frame is frame 1 of the first video of test.list."""
+    lines = [l.strip() for l in open(os.path.join(REF, "sources/data/test.list"))]
+    vi = lines[0]
+    frame = torch.from_numpy(synth.synth_frame(vi.split("/")[0], vi, 1, H, W))[None]
+    out = {"video_info": vi, "frame_id": 1, "H": H, "W": W, "archs": {}}
+    for name in archs:
+        model = getattr(mods["models"], "model_" + name)(num_classes=64)
+        sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+        model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        model.eval()
+        stages = []
+        x = frame
+        with torch.no_grad():
+            for i, child in enumerate(model.convnet.children()):
+                x = child(x)
+                if i >= 3 and len(stages) < 5:  # after maxpool (3), layer1..4 (4..7)
+                    a = x[0].double().numpy()
+                    r = np.random.default_rng(1000 + len(stages)).standard_normal(a.shape)
+                    stages.append(dict(shape=list(a.shape), sum=float(a.sum()), sumsq=float((a * a).sum()),
+                                       absmax=float(np.abs(a).max()), proj=float((a * r).sum())))
+        out["archs"][name] = stages
+    with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(tag, {k: [round(st["sum"], 3) for st in v] for k, v in out["archs"].items()})
+
+
 def make_unreal14_list(path):
     """An UnrealAction-shaped novel split (README.md:23-26: 14 actions, 10 real target videos
     each), in the reference's ``class/video`` list format; names are synthetic."""
@@ -451,11 +482,15 @@ def main():
     ap.add_argument("--only-aug", action="store_true")
     ap.add_argument("--shapes", action="store_true", help="only the config-4 / config-5 shaped episodes")
     ap.add_argument("--preds", type=int, default=0, help="only the N-episode predictions fixture (config 2)")
+    ap.add_argument("--layers", action="store_true", help="only the one-frame per-layer checksums")
     args = ap.parse_args()
     torch.set_num_threads(8)
     _install_stubs()
     gallery_path = os.path.join(tempfile.mkdtemp(), "gallery.list")
     mods = _import_reference(gallery_path)
+    if args.layers:
+        capture_layer_checksums(mods, "layers_one_frame")
+        return
     if args.preds:
         capture_shaped(mods, "resnet18", "protonet", seed=0, episodes=args.preds, tag=f"c2_r18_preds{args.preds}_seed0",
                        n_way=5, k_shot=1, T=16, features=False)
