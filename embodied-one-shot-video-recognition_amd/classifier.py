@@ -8,8 +8,14 @@ int64 [Q] array with the reference's meaning:
   * 'cosine'  : index of the most similar SUPPORT row (classifier.py:117-120).
 Both run in the eosv match kernel.  The reference's protonet accepts exactly one
 query (classifier.py:58 shadows ``query_feature``; Q>1 raises IndexError); here each
-of Q queries is matched against the same support set.  'SVM' / 'KNN' (sklearn, not on
-the north-star path; KNN is broken in the reference) are not provided.
+of Q queries is matched against the same support set.
+  * 'SVM'     : sklearn SVC(C=10) fitted on the support features, on the host, exactly the
+    reference's call (classifier.py:109-111; off the north-star path, the features come from
+    the GPU like the others);
+  * 'KNN'     : raises the reference's NameError (classifier.py:113 reads ``k_shot``, which
+    classifier.py never imports);
+  * anything else: prints 'classifier type error.' and raises the reference's
+    UnboundLocalError (classifier.py:121-122).
 """
 import numpy as np
 import torch
@@ -64,8 +70,13 @@ class Classifier():
             return one_shot_classifier_prototype_lowerdim(data_result)
         if self.classifier == 'cosine':
             return _match(data_result, 'cosine')[0]
-        if self.classifier in ('SVM', 'KNN'):
-            raise NotImplementedError(f"classifier '{self.classifier}' is outside the GPU path "
-                                      "(sklearn; not part of the north-star scope)")
+        if self.classifier == 'SVM':
+            from sklearn.svm import SVC
+
+            classifier_SVM = SVC(C=10)
+            classifier_SVM.fit(_np(data_result['support_feature']), _np(data_result['support_y']))
+            return classifier_SVM.predict(_np(data_result['query_feature']))
+        if self.classifier == 'KNN':
+            raise NameError("name 'k_shot' is not defined")
         print('classifier type error.')
-        return None
+        raise UnboundLocalError("local variable 'predicted_y' referenced before assignment")

@@ -209,14 +209,28 @@ class TestNetwork():
         t = lambda a: torch.from_numpy(np.asarray(a, np.int32)).to(dev)  # noqa: E731
         emb = _engine.clip_embed(feat, t(offs), t(counts), bool(self.L2))
         ns = sup_off[-1]
-        kind = self.classifier if self.classifier in ('protonet', 'cosine') else None
-        if kind is None:
-            raise NotImplementedError(f"classifier {self.classifier!r} is outside the GPU path")
-        pred, _ = _engine.match(emb[ns:].contiguous(), emb[:ns].contiguous(), t(sup_off), t(slots), t(nproto), kind)
+        if self.classifier not in ('protonet', 'cosine'):  # SVM (host sklearn), KNN / unknown: raise as the reference
+            return self._host_classify(emb, sup_off, [np.asarray(p['support_y'], np.float32) for p in plans],
+                                       [p['query_y'] for p in plans])
+        pred, _ = _engine.match(emb[ns:].contiguous(), emb[:ns].contiguous(), t(sup_off), t(slots), t(nproto),
+                                self.classifier)
         debug = getattr(self, 'debug', None)
         if debug is not None:  # tests: per-batch clip embeddings (supports, then queries)
             debug.setdefault('batches', []).append(dict(sup=emb[:ns], q=emb[ns:], sup_off=sup_off, pred=pred))
         return pred.cpu().tolist()
+
+    def _host_classify(self, emb, sup_off, sup_y, query_y):
+        """Classifier.predict per episode on the host (classifier.py:98-123) for the classifiers
+        the match kernel does not run: episode e's supports are rows sup_off[e]..sup_off[e+1]
+        of `emb`, its query row sup_off[-1] + e."""
+        emb = emb.cpu().numpy()
+        ns = sup_off[-1]
+        preds = []
+        for e in range(len(sup_y)):
+            res = {'support_feature': emb[sup_off[e]:sup_off[e + 1]], 'support_y': sup_y[e],
+                   'query_feature': emb[ns + e:ns + e + 1], 'query_y': np.array([query_y[e]], np.float32)}
+            preds.append(int(np.asarray(self.myClassifier.predict(res)).reshape(-1)[0]))
+        return preds
 
     def _baseline_per_episode(self, n):
         accs = []
@@ -364,10 +378,10 @@ class TestNetwork():
                 slots += [sl_] * (ns_v + 1)
             nproto.append(len(seen))
             off.append(off[-1] + nk * (ns_v + 1))
-        kind = self.classifier if self.classifier in ('protonet', 'cosine') else None
-        if kind is None:
-            raise NotImplementedError(f"classifier {self.classifier!r} is outside the GPU path")
-        pred, _ = _engine.match(q_emb, sup.contiguous(), t(off), t(slots), t(nproto), kind)
+        if self.classifier not in ('protonet', 'cosine'):  # SVM (host sklearn), KNN / unknown: raise as the reference
+            sup_y = [np.repeat(np.asarray(p['support_y'], np.float32), ns_v + 1) for p in plans]
+            return self._host_classify(torch.cat([sup, q_emb]), off, sup_y, [p['query_y'] for p in plans])
+        pred, _ = _engine.match(q_emb, sup.contiguous(), t(off), t(slots), t(nproto), self.classifier)
         if debug is not None:
             debug.update(seg=seg, pool=pool, sup=sup, q_emb=q_emb, pred=pred)
         return pred.cpu().tolist()

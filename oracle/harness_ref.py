@@ -123,6 +123,12 @@ def predict(kind: str, support_feature, support_y, query_feature, query_y):
         return protonet_predict(support_feature, support_y, query_feature, query_y)[0]
     if kind == "cosine":
         return cosine_predict(support_feature, query_feature)[0]
+    if kind == "SVM":  # classifier.py:109-111
+        from sklearn.svm import SVC
+
+        clf = SVC(C=10)
+        clf.fit(support_feature, support_y)
+        return clf.predict(query_feature)
     raise ValueError(kind)
 
 

@@ -483,6 +483,7 @@ def main():
     ap.add_argument("--shapes", action="store_true", help="only the config-4 / config-5 shaped episodes")
     ap.add_argument("--preds", type=int, default=0, help="only the N-episode predictions fixture (config 2)")
     ap.add_argument("--layers", action="store_true", help="only the one-frame per-layer checksums")
+    ap.add_argument("--svm", action="store_true", help="only the SVM-classifier baseline episodes")
     args = ap.parse_args()
     torch.set_num_threads(8)
     _install_stubs()
@@ -490,6 +491,9 @@ def main():
     mods = _import_reference(gallery_path)
     if args.layers:
         capture_layer_checksums(mods, "layers_one_frame")
+        return
+    if args.svm:
+        capture_baseline(mods, "resnet18", "SVM", seed=5, episodes=8, tag="c1_r18_svm_seed5")
         return
     if args.preds:
         capture_shaped(mods, "resnet18", "protonet", seed=0, episodes=args.preds, tag=f"c2_r18_preds{args.preds}_seed0",
@@ -513,6 +517,8 @@ def main():
         capture_baseline(mods, "resnet18", "protonet", seed=1, episodes=20, tag="c1_r18_protonet_seed1")
         capture_baseline(mods, "resnet18", "cosine", seed=2, episodes=6, tag="c1_r18_cosine_seed2")
         capture_baseline(mods, "resnet50", "protonet", seed=3, episodes=3, tag="c1_r50_protonet_seed3")
+    if not args.only_aug:
+        capture_baseline(mods, "resnet18", "SVM", seed=5, episodes=8, tag="c1_r18_svm_seed5")
     if args.aug or args.only_aug:
         capture_aug(mods, seed=4, episodes=2, tag="c3_r50_aug_seed4")
 

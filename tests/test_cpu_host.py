@@ -265,3 +265,24 @@ def test_asan_host_plan_service_matches_library(n_way, k_shot, seed, n, sizes):
         return
     want = " ".join(" ".join(map(str, [*cls[e], *q[e], *sup[e].reshape(-1)[:n_way * k_shot]])) for e in range(n))
     assert r.stdout.split() == want.split()
+
+
+def test_dropin_classifier_host_kinds_follow_reference():
+    """classifier.py:98-123 for the kinds the match kernel does not run: 'SVM' is sklearn's
+    SVC(C=10) on the host, equal to the oracle's restatement on the SVM fixture's own reference
+    embeddings; 'KNN' raises the reference's NameError (k_shot is never imported there);
+    an unknown kind prints and raises UnboundLocalError."""
+    import classifier
+    from oracle import harness_ref
+
+    meta, arr = load_fixture("c1_r18_svm_seed5")
+    for e, ep in enumerate(meta["episodes"]):
+        d = {"support_feature": arr["support_feature"][e], "support_y": np.array(ep["support_y"], np.float32),
+             "query_feature": arr["query_feature"][e], "query_y": np.array([ep["query_y"]], np.float32)}
+        got = classifier.Classifier("SVM").predict(d)
+        ref = harness_ref.predict("SVM", d["support_feature"], d["support_y"], d["query_feature"], d["query_y"])
+        assert np.array_equal(got, ref) and int(got[0]) == int(arr["pred"][e][0])
+    with pytest.raises(NameError, match="k_shot"):
+        classifier.Classifier("KNN").predict(d)
+    with pytest.raises(UnboundLocalError):
+        classifier.Classifier("LR").predict(d)

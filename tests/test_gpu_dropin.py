@@ -39,7 +39,8 @@ def test_models_dropin_forward(name):
     assert list(m.state_dict().keys()) == list(ref.state_dict().keys())
 
 
-@pytest.mark.parametrize("tag", ["c1_r18_protonet_seed1", "c1_r18_cosine_seed2", "c1_r50_protonet_seed3"])
+@pytest.mark.parametrize("tag", ["c1_r18_protonet_seed1", "c1_r18_cosine_seed2", "c1_r50_protonet_seed3",
+                                 "c1_r18_svm_seed5"])
 def test_network_test_baseline_reproduces_reference_file(tag, tmp_path):
     import network_test
     import utils
@@ -165,3 +166,28 @@ def test_aug_segment_feature_gather_equals_reforward(tmp_path, monkeypatch):
     assert torch.equal(a["sup"], b["sup"])
     assert torch.equal(a["q_emb"], b["q_emb"])
     assert torch.equal(a["pred"], b["pred"]) and acc_a == acc_b
+
+
+def test_aug_segment_with_svm_classifier(tmp_path, monkeypatch):
+    """aug_seg_T with classifier='SVM' (host sklearn on the GPU's augmented support set,
+    network_test.py:251-255 -> classifier.py:109-111): the predictions equal SVC(C=10) fitted
+    on the reference's own augmented features of the C3 fixture."""
+    import generate_augmented_datasets as gad
+    import network_test
+    import utils
+
+    meta, arr = load_fixture("c3_r50_aug_seed4")
+    pkl = str(tmp_path / "model.pkl")
+    _save_sd("resnet50", pkl)
+    monkeypatch.setattr(utils, "GALLERY_LIST", str(tmp_path / "gallery.list"))
+    monkeypatch.setitem(utils.EPISODE_NUMS, "test", len(meta["episodes"]))
+    random.seed(meta["seed"])
+    np.random.seed(meta["seed"])
+    gad.generate_gallery_list()
+    tn = network_test.TestNetwork(str(tmp_path / "acc.txt"), "resnet50", "SVM", True)
+    tn.test_network_aug_segment(pre_model=pkl)
+    tn.acc_file.close()
+    for e, ep in enumerate(meta["episodes"]):
+        ref = harness_ref.predict("SVM", arr["aug_features"][e], arr["aug_labels"][e], arr["query_feature"][e],
+                                  np.array([ep["query_y"]], np.float32))
+        assert tn.last_accs[e] == float(int(ref[0]) == ep["query_y"])
