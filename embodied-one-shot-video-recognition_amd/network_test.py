@@ -382,6 +382,7 @@ class TestNetwork():
             sup_y = [np.repeat(np.asarray(p['support_y'], np.float32), ns_v + 1) for p in plans]
             return self._host_classify(torch.cat([sup, q_emb]), off, sup_y, [p['query_y'] for p in plans])
         pred, _ = _engine.match(q_emb, sup.contiguous(), t(off), t(slots), t(nproto), self.classifier)
-        if debug is not None:
-            debug.update(seg=seg, pool=pool, sup=sup, q_emb=q_emb, pred=pred)
+        if debug is not None:  # concatenated over batches, in episode order
+            for k, v in dict(seg=seg, pool=pool, sup=sup, q_emb=q_emb, pred=pred).items():
+                debug[k] = torch.cat([debug[k], v]) if k in debug else v
         return pred.cpu().tolist()

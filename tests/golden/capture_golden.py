@@ -262,7 +262,26 @@ def capture_plans(mods, seed, episodes, tag):
     print(tag, len(out))
 
 
-def capture_aug(mods, seed, episodes, tag):
+def compact_aug(npz_path):
+    """Shrink a config-3 fixture for many episodes: the pool ids, each row's 16 smallest smoothed
+    distances (indices + values; a lower-precision pick outside them fails its test), and the
+    augmented features as projections onto a fixed N(0,1) vector (default_rng(20261017)) instead
+    of the [E,45,2048] features and [E,40,5120] distances."""
+    a = dict(np.load(npz_path))
+    sm = a.pop("smoothed")
+    a.pop("distance_row0", None)
+    order = np.argsort(sm, axis=2, kind="stable")
+    a["pool"] = order[:, :, 0].astype(np.int16)
+    a["top16_idx"] = order[:, :, :16].astype(np.int16)
+    a["top16_val"] = np.take_along_axis(sm, order[:, :, :16], axis=2).astype(np.float32)
+    feats = a.pop("aug_features").astype(np.float64)
+    r = np.random.default_rng(20261017).standard_normal(feats.shape[-1])
+    a["aug_proj"] = feats @ r
+    a["aug_absmax"] = np.abs(feats).max(axis=2)
+    np.savez_compressed(npz_path, **a)
+
+
+def capture_aug(mods, seed, episodes, tag, compact=False):
     """test_network_aug_segment (config 3 path), R50, fp32 CPU."""
     utils = mods["utils"]
     utils.EPISODE_NUMS["test"] = episodes
@@ -309,6 +328,8 @@ def capture_aug(mods, seed, episodes, tag):
                         pred=np.stack([p["pred"] for p in rec.predicts]).astype(np.int64),
                         distance_row0=np.stack([q["distance"][0] for q in pool]),
                         smoothed=np.stack([q["smoothed"] for q in pool]).astype(np.float32))
+    if compact:
+        compact_aug(os.path.join(OUT, f"{tag}.npz"))
     with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
         json.dump(dict(arch="resnet50", classifier="protonet", seed=seed, episodes=eps,
                        gallery=gal["lines"], acc_file=acc_text), f, indent=1)
@@ -484,6 +505,7 @@ def main():
     ap.add_argument("--preds", type=int, default=0, help="only the N-episode predictions fixture (config 2)")
     ap.add_argument("--layers", action="store_true", help="only the one-frame per-layer checksums")
     ap.add_argument("--svm", action="store_true", help="only the SVM-classifier baseline episodes")
+    ap.add_argument("--aug-seed6", action="store_true", help="only the 8-episode config-3 fixture")
     args = ap.parse_args()
     torch.set_num_threads(8)
     _install_stubs()
@@ -494,6 +516,9 @@ def main():
         return
     if args.svm:
         capture_baseline(mods, "resnet18", "SVM", seed=5, episodes=8, tag="c1_r18_svm_seed5")
+        return
+    if args.aug_seed6:
+        capture_aug(mods, seed=6, episodes=8, tag="c3_r50_aug_seed6", compact=True)
         return
     if args.preds:
         capture_shaped(mods, "resnet18", "protonet", seed=0, episodes=args.preds, tag=f"c2_r18_preds{args.preds}_seed0",
@@ -521,6 +546,7 @@ def main():
         capture_baseline(mods, "resnet18", "SVM", seed=5, episodes=8, tag="c1_r18_svm_seed5")
     if args.aug or args.only_aug:
         capture_aug(mods, seed=4, episodes=2, tag="c3_r50_aug_seed4")
+        capture_aug(mods, seed=6, episodes=8, tag="c3_r50_aug_seed6", compact=True)
 
 
 if __name__ == "__main__":

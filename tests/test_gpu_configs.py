@@ -124,12 +124,12 @@ def test_five_shot_prototypes_through_native_match():
 
 
 # ---------------------------------------------------------------------------------- config 3
-def _run_c3(tmp_path, monkeypatch, dtype):
+def _run_c3(tmp_path, monkeypatch, dtype, tag="c3_r50_aug_seed4"):
     import generate_augmented_datasets as gad
     import network_test
     import utils
 
-    meta, arr = load_fixture("c3_r50_aug_seed4")
+    meta, arr = load_fixture(tag)
     pkl = str(tmp_path / "model.pkl")
     _save_sd("resnet50", pkl)
     monkeypatch.setattr(utils, "GALLERY_LIST", str(tmp_path / "gallery.list"))
@@ -173,5 +173,40 @@ def test_aug_segment_fast_legs(dtype, tmp_path, monkeypatch):
     q = dbg["q_emb"].cpu().numpy()
     tol = 1e-2 if dtype == "bf16" else 1e-4
     assert _rel(q, arr["query_feature"][:, 0]) < tol
+    assert np.array_equal(dbg["pred"].cpu().numpy(), arr["pred"][:, 0])
+    assert acc_text == meta["acc_file"]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f32x3", "bf16"])
+def test_aug_segment_eight_reference_episodes(dtype, tmp_path, monkeypatch):
+    """Config 3 over 8 more reference episodes (320 gallery matches; compact fixture: pool ids,
+    each row's 16 smallest reference smoothed distances, augmented-feature projections).
+    f32: pool ids identical.  f32x3 / bf16: where a pick differs it is among the reference's 16
+    nearest and within delta (1e-4 / 1e-2, relative) of the row's minimum.  Augmented features
+    within 1e-4 (f32, f32x3) / 1e-2 (bf16) through the projection bound; predictions and the
+    result file identical."""
+    dbg, acc_text, meta, arr = _run_c3(tmp_path, monkeypatch, dtype, tag="c3_r50_aug_seed6")
+    E = len(meta["episodes"])
+    ref_pool = arr["pool"].astype(np.int64)
+    got_pool = dbg["pool"].cpu().numpy().reshape(E, -1)
+    same = got_pool == ref_pool
+    delta = 1e-4 if dtype != "bf16" else 1e-2
+    best = arr["top16_val"][:, :, 0]
+    worst_slack = 0.0
+    for e, s_ in zip(*np.nonzero(~same)):
+        hit = np.flatnonzero(arr["top16_idx"][e, s_] == got_pool[e, s_])
+        assert hit.size, f"episode {e} segment {s_}: pick {got_pool[e, s_]} outside the reference's 16 nearest"
+        slack = (arr["top16_val"][e, s_, hit[0]] - best[e, s_]) / abs(best[e, s_])
+        worst_slack = max(worst_slack, float(slack))
+    print(f"[c3 x{E} {dtype}] pool-id agreement {same.mean():.3f}, max relative slack {worst_slack:.2e}")
+    if dtype == "f32":
+        assert same.all()
+    assert worst_slack <= delta
+    sup = dbg["sup"].cpu().numpy().astype(np.float64).reshape(E, 45, -1)
+    D = sup.shape[-1]
+    r = np.random.default_rng(20261017).standard_normal(D)
+    tol = 1e-4 if dtype != "bf16" else 1e-2
+    bound = tol * np.sqrt(D) * arr["aug_absmax"] * np.linalg.norm(r)
+    assert (np.abs(sup @ r - arr["aug_proj"]) <= bound).all()
     assert np.array_equal(dbg["pred"].cpu().numpy(), arr["pred"][:, 0])
     assert acc_text == meta["acc_file"]
