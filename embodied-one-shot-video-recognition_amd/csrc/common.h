@@ -127,6 +127,8 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
                          LaunchInfo* info = nullptr);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
+bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
+int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_x3(const ConvArgs& a, hipStream_t s);
 

@@ -322,6 +322,9 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_dma<128, 64, 16, 2, 2, true>(a, s);
+  // stage-1 3x3 64->64 convs: row-strip direct conv (input staged once per strip, not per tap)
+  static const int rows = env_switch("EOSV_F32_ROWS", 1);  // 0 = implicit GEMM (A/B switch)
+  if (rows && conv_rows_f32_ok(a)) return launch_conv_rows_f32(a, s);
   if (a.Cout % 4) {
     if (a.x2) return set_error("conv_f32: fused downsample needs Cout % 4 == 0"), EOSV_ERR_UNSUPPORTED;
     return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);

@@ -464,6 +464,12 @@ int main() {
   // f32 stride-1 3x3 convs at the stage shapes of R18/R50, the fused downsample (K columns
   // [K1, K) from x2), ragged maps and M tails; exact-f32 products, so a tight bound
   fails += check(12, 56, 56, 64, 64, 3, 1, 1, false, true, true, 0, 2e-6);
+  // f32 stage-1 row-strip kernel (conv_rows_f32.hip): 560 strips (2-3 per workgroup), R50's
+  // residual-free conv, 64-wide maps (256x256 input), no ReLU
+  fails += check(20, 56, 56, 64, 64, 3, 1, 1, false, true, true, 0, 2e-6);
+  fails += check(3, 56, 56, 64, 64, 3, 1, 1, false, false, true, 0, 2e-6);
+  fails += check(4, 64, 64, 64, 64, 3, 1, 1, false, true, true, 0, 2e-6);
+  fails += check(2, 64, 64, 64, 64, 3, 1, 1, false, false, false, 0, 2e-6);
   fails += check(5, 28, 28, 128, 128, 3, 1, 1, false, false, true, 64, 2e-6);
   fails += check(6, 14, 14, 256, 256, 3, 1, 1, false, true, true, 0, 2e-6);
   fails += check(4, 14, 14, 256, 256, 3, 1, 1, false, false, true, 128, 2e-6);
