@@ -330,6 +330,14 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
     return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);
   }
   if (a.Cout <= 64) return launch_dma<256, 64, 16, 4, 1, false>(a, s);
+#ifdef EOSV_PROFILING
+  // A/B of the Cout >= 128 tiles: 1 BK 32, 2 three-deep ring, 3 128x128 everywhere, 4 256x256 at Cout >= 256
+  static const int tile = env_switch("EOSV_F32_TILE", 0);
+  if (tile == 1) return a.Cout <= 256 ? launch_dma<256, 128, 32, 4, 2, false>(a, s) : launch_dma<128, 128, 32, 2, 2, false>(a, s);
+  if (tile == 2) return a.Cout <= 256 ? launch_dma<256, 128, 16, 4, 2, false, 3>(a, s) : launch_dma<128, 128, 16, 2, 2, false, 3>(a, s);
+  if (tile == 3) return launch_dma<128, 128, 16, 2, 2, false>(a, s);
+  if (tile == 4 && a.Cout >= 256) return launch_dma<256, 256, 16, 4, 2, false>(a, s);
+#endif
   if (a.Cout <= 256) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
   return launch_dma<128, 128, 16, 2, 2, false>(a, s);
 }

@@ -434,6 +434,7 @@ int main() {
   fails += check_stem_pool_f32(3, 100, 86);
   fails += check_stem_pool_f32(2, 64, 48);
   fails += check_stem_pool_f32(2, 40, 200);  // Ws 100: a partial last column tile
+  fails += check_stem_pool_f32(2, 256, 256);  // 8 column tiles
   // stage-1 shape (row-strip kernel): 300 images = 4200 strips, several strips per workgroup
   fails += check_bf16(300, 56, 56, 64, 64, 3, 1, 1, true, true);
   fails += check_bf16(3, 56, 56, 64, 64, 3, 1, 1, false, true);
