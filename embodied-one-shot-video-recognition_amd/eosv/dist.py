@@ -54,6 +54,36 @@ def gather_predictions(local_idx: Sequence[int], local_pred: Sequence[int], n_to
     return preds
 
 
+def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
+    """Every rank's rows of ``x`` ([n_r, ...], any n_r), concatenated in rank order, on x's device.
+
+    Used by the config-3 driver to shard the gallery forward: rank r computes a
+    contiguous block of gallery videos and one all-gather (RCCL over xGMI, or gloo through the
+    host) rebuilds the full per-frame feature table on every rank.  The backbone computes every
+    frame independently of its batch, so the table is bit-identical to the unsharded one."""
+    d, _, n_ranks = world()
+    if d is None or n_ranks == 1:
+        return x
+    dev = _coll_device(d)
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(n) for _ in range(n_ranks)]
+    d.all_gather(ns, n)
+    ns = [int(v.item()) for v in ns]
+    m = max(ns)
+    buf = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
+    buf[:x.shape[0]] = x.to(dev)
+    parts = [torch.empty_like(buf) for _ in range(n_ranks)]
+    d.all_gather(parts, buf)
+    return torch.cat([p[:k] for p, k in zip(parts, ns)]).to(x.device)
+
+
+def block_range(n: int, rank: int, n_ranks: int):
+    """Contiguous block [lo, hi) of n items for rank (the first n % n_ranks ranks take one more)."""
+    q, r = divmod(n, n_ranks)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (rank < r)
+
+
 def max_over_ranks(x: float) -> float:
     d, _, _ = world()
     if d is None:

@@ -258,16 +258,22 @@ class TestNetwork():
         T, sl = utils.VIDEO_FRAMES, utils.seg_len
         dev = torch.device('cuda', torch.cuda.current_device())
         infos = _gad.gallery_video_infos()
+        clips_all = []
+        for vi in infos:  # every rank checks every video, so a bad list fails on all ranks alike
+            ids = self._ids(vi, 'test')
+            if len(ids) != T:
+                raise ValueError(f"gallery video {vi} has {len(ids)} < {T} frames "
+                                 "(the reference's torch.stack fails on it too)")
+            clips_all.append((vi, ids, T))
         feats, raws = [], []
         self._gallery_frames = [] if self._aug_reforward() else None
-        for g0 in range(0, len(infos), 64):
-            clips = []
-            for vi in infos[g0:g0 + 64]:
-                ids = self._ids(vi, 'test')
-                if len(ids) != T:
-                    raise ValueError(f"gallery video {vi} has {len(ids)} < {T} frames "
-                                     "(the reference's torch.stack fails on it too)")
-                clips.append((vi, ids, T))
+        # multi-rank: each rank forwards a contiguous block of the gallery videos and one
+        # all-gather rebuilds the table; the re-forward mode keeps every frame local
+        _, rank, world = _dist()
+        lo, hi = (0, len(clips_all)) if self._gallery_frames is not None else _dist_mod.block_range(
+            len(clips_all), rank, world)
+        for g0 in range(lo, hi, 64):
+            clips = clips_all[g0:min(g0 + 64, hi)]
             fr = self._clip_frames(clips, H, W, dev)
             if self._gallery_frames is not None:
                 self._gallery_frames.append(fr)
@@ -278,8 +284,11 @@ class TestNetwork():
                 f = _engine.clip_embed(f, torch.arange(n, dtype=torch.int32, device=dev),
                                        torch.ones(n, dtype=torch.int32, device=dev), True)
             feats.append(f)
-        feat = torch.cat(feats)
-        raw = torch.cat(raws)
+        D = self._backbone(H, W).D
+        feat = torch.cat(feats) if feats else torch.empty((0, D), device=dev)
+        raw = torch.cat(raws) if raws else torch.empty((0, D), device=dev)
+        if self._gallery_frames is None:
+            feat, raw = _dist_mod.all_gather_rows(feat), _dist_mod.all_gather_rows(raw)
         if feat.shape[1] != 2048:
             raise ValueError("test_network_aug_segment needs a 2048-d backbone (resnet50/101): the reference "
                              "np.resize's features to 2048 (network_test.py:188,204)")

@@ -145,8 +145,13 @@ preds = edist.gather_predictions(mine, fake, len(plans))
 accs = edist.episode_accs(preds, [p["query_y"] for p in plans])
 t = edist.max_over_ranks(float(rank + 1))
 n = edist.sum_over_ranks(len(mine))
+# the config-3 gallery shard: 37 "videos" in contiguous blocks, one all-gather of their rows
+lo, hi = edist.block_range(37, rank, world)
+rows = torch.arange(lo * 3, hi * 3, dtype=torch.float32).view(-1, 3)
+table = edist.all_gather_rows(rows)
 if rank == 0:
-    print(json.dumps({"preds": preds.tolist(), "accs": [float(a) for a in accs], "t": t, "n": n}))
+    print(json.dumps({"preds": preds.tolist(), "accs": [float(a) for a in accs], "t": t, "n": n,
+                      "table": table.tolist()}))
 dist.destroy_process_group()
 """
 
@@ -171,6 +176,7 @@ def test_episode_sharding_gloo(world, tmp_path):
     plans = episodes.sample_episodes(37, 5, 1, "test", seed=11)
     assert res["accs"] == [float(p["query_y"] == e) for p, e in zip(plans, expect)]
     assert res["t"] == float(world) and res["n"] == 37
+    assert res["table"] == np.arange(37 * 3, dtype=np.float32).reshape(37, 3).tolist()
 
 
 def test_jpeg_clip_window_draws_follow_reference_order(tmp_path):

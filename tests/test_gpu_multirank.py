@@ -4,6 +4,9 @@ one device.  RCCL refuses two ranks on one GPU, so these run the same code over 
 
 * the drop-in TestNetwork.test_network_baseline over 2 ranks writes the reference's result file
   byte for byte (network_test.py:132-167);
+* the config-3 driver (test_network_aug_segment) over 2 ranks: each rank forwards half of the
+  640 gallery videos and one all-gather rebuilds the table; the result file, pool ids and
+  augmented embeddings equal the 1-rank run's fixture (network_test.py:170-267, SURVEY 8(e));
 * ``bench.py --gpus 2`` spawns its own ranks (no launcher), reports n_gpus = 2 and the same
   episode accuracy as the 1-rank run over the same timed episodes.
 """
@@ -12,6 +15,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from _common import load_fixture
@@ -67,6 +71,63 @@ def test_dropin_baseline_two_ranks_writes_reference_file(tag, tmp_path):
     _spawn([sys.executable, str(script), PKG, REPO, tag, out], 2, 29611 + os.getpid() % 500)
     meta, _ = load_fixture(tag)
     assert open(out).read() == meta["acc_file"]
+
+
+_DROPIN_AUG = r"""
+import os, random, sys
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+rank = dist.get_rank()
+import generate_augmented_datasets as gad, network_test, utils
+from eosv import arch, synth
+tag, out = sys.argv[3], sys.argv[4]
+import json
+meta = json.load(open(os.path.join(sys.argv[2], "tests", "golden", tag + ".json")))
+utils.EPISODE_NUMS["test"] = len(meta["episodes"])
+utils.GALLERY_LIST = out + f".gallery{rank}.list"
+pkl = out + ".model.pkl"
+if rank == 0:
+    sd = synth.synth_state_dict(arch.SPECS["resnet50"], 64, 0)
+    torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, pkl)
+dist.barrier()
+random.seed(meta["seed"]); np.random.seed(meta["seed"])
+gad.generate_gallery_list()
+assert gad.gallery_video_infos() == meta["gallery"]
+tn = network_test.TestNetwork(out, "resnet50", "protonet", True)
+tn.mymodel.compute_dtype = "f32"
+tn.debug = {}
+tn.test_network_aug_segment(pre_model=pkl)
+if rank == 0:
+    tn.acc_file.close()
+np.savez(out + f".rank{rank}.npz", pool=tn.debug["pool"].cpu().numpy(), sup=tn.debug["sup"].cpu().numpy(),
+         seg_sum=float(tn._gallery_raw.double().sum()), n_gal=tn._gallery_raw.shape[0])
+dist.destroy_process_group()
+"""
+
+
+def test_aug_segment_two_ranks_shard_the_gallery(tmp_path):
+    """Episodes e % 2 == r on rank r, the gallery forward split in two contiguous halves."""
+    tag = "c3_r50_aug_seed6"
+    script = tmp_path / "aug.py"
+    script.write_text(_DROPIN_AUG)
+    out = str(tmp_path / "acc.txt")
+    _spawn([sys.executable, str(script), PKG, REPO, tag, out], 2, 29811 + os.getpid() % 500, timeout=300)
+    meta, arr = load_fixture(tag)
+    assert open(out).read() == meta["acc_file"]
+    r0, r1 = (np.load(out + f".rank{r}.npz") for r in (0, 1))
+    assert int(r0["n_gal"]) == int(r1["n_gal"]) == 640 * 16 and float(r0["seg_sum"]) == float(r1["seg_sum"])
+    E = len(meta["episodes"])
+    ref_pool = arr["pool"].astype(np.int64)
+    for r, res in ((0, r0), (1, r1)):  # rank r ran episodes r, r + 2, ...
+        got = res["pool"].reshape(-1, ref_pool.shape[1])
+        assert np.array_equal(got, ref_pool[r::2]), r
+        sup = res["sup"].astype(np.float64).reshape(-1, 45, 2048)
+        rv = np.random.default_rng(20261017).standard_normal(2048)
+        bound = 1e-4 * np.sqrt(2048) * arr["aug_absmax"][r::2] * np.linalg.norm(rv)
+        assert (np.abs(sup @ rv - arr["aug_proj"][r::2]) <= bound).all()
+    assert E == 8
 
 
 def _bench(extra_env, gpus, eps):
