@@ -67,7 +67,7 @@ __device__ __forceinline__ float row_ror1(float v) {
 // y: [N][Hq][Wq][64] f32 (pooled).  Grid = N images, block = 256 threads, NT = ceil(Ws / 16).
 // SPLIT (EOSV_F32X3): y is [N][Hq][Wq][128] bf16, (hi, lo) of each pooled f32 value.
 template <bool SPLIT, int NT>
-__global__ __launch_bounds__(SPF_NT, 2) void stem_pool_f32_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ bias, void* y, int H,
                                                                  int W, int Hs, int Ws, int Hq, int Wq) {
