@@ -197,10 +197,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
     }
     // the next slot's DMA must have landed (leave the newest stage in flight when NS == 3),
     // and every wave's reads of this slot must be done before anyone refills it
-    if (NS == 3 && issue)
+    if (EOSV_ABL(a) & 4) {
+      // profiling: DMA issued but not waited for (results wrong)
+    } else if (NS == 3 && issue) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
-    else
+    } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     slot = slot + 1 == NS ? 0 : slot + 1;
