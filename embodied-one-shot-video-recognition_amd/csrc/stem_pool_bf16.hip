@@ -333,7 +333,12 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
 // is its first: the left edge of pooled column 28c's window); a lane's k = its stem column
 // relative to that, + 1, so byte 12k of the row starts the lane's 7-pixel run, as before.
 constexpr int CB_TILES = 4;
-constexpr int CB_CH = (168 * CB_TILES + 72 + 15) / 16;  // 16-B chunks per ring copy (47)
+// 16-B chunks per ring copy: 51, not the 47 the row needs.  Lane k (stem column, k = 4a + m)
+// reads chunk m * CB_CH + 3a + m (+ c): with CB_CH = 47 that is 48m + 3a + c, the same bank
+// group for the 4 lanes of one a (SQ_LDS_BANK_CONFLICT at 40 % of the stem's CU cycles, r02);
+// CB_CH + 1 = 52 = 4 (mod 16) spreads the 16 lanes of a row over all 16 bank groups.
+constexpr int CB_CH = 51;
+static_assert((CB_CH + 1) % 16 == 4 && CB_CH * 16 >= 168 * CB_TILES + 72, "conflict-free B-fragment reads");
 constexpr int CB_GP = 14 * CB_TILES + 5;               // column pairs per ring row (61)
 constexpr int CB_STG = 128;                             // f32 per staged plane row (32 lanes x 4)
 constexpr int CB_LDS = RING * 4 * CB_CH * 16;
