@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
         if (++nkw == a.KW) nkw = 0, ++nkh;
       }
 #pragma unroll
-      for (int j = 0; j < AI; ++j) {
+      for (int j = 0; j < ((EOSV_ABL(a) & 8) ? 0 : AI); ++j) {  // profiling: 8 = no A-tile DMA
         const int ih = aih[j] + kh, iw = aiw[j] + kw;
         const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const float* src = ok ? arow[j] + toff : zero;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
       }
     }
 #pragma unroll
-    for (int j = 0; j < BI; ++j) {
+    for (int j = 0; j < ((EOSV_ABL(a) & 16) ? 0 : BI); ++j) {  // profiling: 16 = no B-tile DMA
       const float* src = brow[j] ? brow[j] + k0 : zero;
       float* dst = Bs + (wid * (BN / NW) + RPI * j) * BK;
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
