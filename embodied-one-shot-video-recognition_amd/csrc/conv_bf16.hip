@@ -423,6 +423,16 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   // tile.  r01 A/B (tools/ab_sets.sh): 12-15 % faster than a phased 8-wave 512x128 kernel (whose 8
   // barriers per K-tile cost more than its overlap gains: SQ MFMA-busy 0.29 vs 0.42) and 5 %
   // faster than 128x128 on the stride-2 entry.
+#ifdef EOSV_PROFILING
+  // A/B of the Cout-128 tile for the stride-2 entries / 1x1s (not the tap-shift convs):
+  // 1 256x128 (8 waves), 2 128x128 (4 waves), 3 256x128 (4 waves); bit 4: f32x3 (split) only
+  static const int s2t = env_switch("EOSV_BF16_C128_TILE", 0);
+  if (a.Cout == 128 && (s2t & 3) && (!(s2t & 4) || a.split)) {
+    if ((s2t & 3) == 1) return launch_bf16<256, 128, 4, 2, false>(a, s);
+    if ((s2t & 3) == 2) return launch_bf16<128, 128, 2, 2, false>(a, s);
+    return launch_bf16<256, 128, 2, 2, false>(a, s);
+  }
+#endif
   if (a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
   if (a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
   return launch_bf16<128, 64, 2, 2, false>(a, s);
