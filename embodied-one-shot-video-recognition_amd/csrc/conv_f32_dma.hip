@@ -340,6 +340,8 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
   if (tile == 2) return a.Cout <= 256 ? launch_dma<256, 128, 16, 4, 2, false, 3>(a, s) : launch_dma<128, 128, 16, 2, 2, false, 3>(a, s);
   if (tile == 3) return launch_dma<128, 128, 16, 2, 2, false>(a, s);
   if (tile == 4 && a.Cout >= 256) return launch_dma<256, 256, 16, 4, 2, false>(a, s);
+  if (tile == 5) return launch_dma<512, 128, 16, 4, 2, false>(a, s);  // 8 waves of 128x64
+  if (tile == 6 && a.Cout <= 256) return launch_dma<512, 128, 16, 4, 2, false>(a, s);
 #endif
   if (a.Cout <= 256) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
   return launch_dma<128, 128, 16, 2, 2, false>(a, s);
