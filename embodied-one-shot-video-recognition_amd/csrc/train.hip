@@ -1,0 +1,530 @@
+// Training path: the pieces TrainNetwork.finetune_model needs on top of the
+// inference kernels (reference network_train.py:52-131: ResNet in train mode, batch-statistics
+// BN, fc + CrossEntropyLoss, loss.backward(), SGD with momentum on convnet and fc).
+//
+// The conv GEMMs of a training step (forward Y = Xcol . W^T, input gradient dXcol = dY . W,
+// weight gradient dW = dY^T . Xcol) are plain f32 GEMMs over an explicit im2col buffer
+// (288 GB of HBM holds the largest, R50 stem at 96 frames: 0.8 GB), so they go to rocBLAS
+// (atomics off: deterministic).  Everything around them is here: im2col / col2im (gather,
+// deterministic), batch-norm forward with batch statistics and running-stat update, its
+// backward with the ReLU mask and the residual branch fused, max-pool with argmax indices and
+// its gather backward, average pool, softmax cross-entropy, SGD with momentum.
+// Layouts: activations NHWC f32 ([P][C] rows, P = N*H*W), conv weights [Cout][KH][KW][Cin].
+#include <rocblas/rocblas.h>
+
+#include <mutex>
+
+#include "common.h"
+
+namespace eosv {
+namespace {
+
+constexpr int BN_CHUNKS = 256;  // row chunks of the two-stage per-channel reductions
+
+int grid_for(long long n, int block = 256) {
+  const long long g = (n + block - 1) / block;
+  return (int)std::min<long long>(std::max<long long>(g, 1), 1 << 20);
+}
+
+__global__ void im2col_kernel(const float* __restrict__ x, int N, int H, int W, int C, int KH, int KW, int stride,
+                              int pad, int Ho, int Wo, float* __restrict__ col) {
+  const long long K = (long long)KH * KW * C;
+  const long long total = (long long)N * Ho * Wo * K;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long p = i / K;
+    const int k = (int)(i - p * K);
+    const int c = k % C, t = k / C, kw = t % KW, kh = t / KW;
+    const int ow = (int)(p % Wo);
+    const long long r = p / Wo;
+    const int oh = (int)(r % Ho), n = (int)(r / Ho);
+    const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+    col[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                 ? x[(((long long)n * H + ih) * W + iw) * C + c]
+                 : 0.f;
+  }
+}
+
+// dx[n][ih][iw][c] = sum over the taps that read it of dcol[(n, oh, ow)][(kh, kw, c)]
+__global__ void col2im_kernel(const float* __restrict__ col, int N, int H, int W, int C, int KH, int KW, int stride,
+                              int pad, int Ho, int Wo, float* __restrict__ dx) {
+  const long long K = (long long)KH * KW * C;
+  const long long total = (long long)N * H * W * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long r = i / C;
+    const int iw = (int)(r % W);
+    const long long r2 = r / W;
+    const int ih = (int)(r2 % H), n = (int)(r2 / H);
+    float s = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int th = ih + pad - kh;
+      if (th < 0 || th % stride) continue;
+      const int oh = th / stride;
+      if (oh >= Ho) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int tw = iw + pad - kw;
+        if (tw < 0 || tw % stride) continue;
+        const int ow = tw / stride;
+        if (ow >= Wo) continue;
+        s += col[(((long long)n * Ho + oh) * Wo + ow) * K + ((long long)kh * KW + kw) * C + c];
+      }
+    }
+    dx[i] = s;
+  }
+}
+
+// per (row chunk, channel): partial sums in double.  MODE 0: x, x^2.  MODE 1 (backward): g, g*xhat
+// with g = dy masked by y > 0 when relu (and written to dres when given)
+template <int MODE>
+__global__ void bn_partials_kernel(const float* __restrict__ a, const float* __restrict__ dy, const float* __restrict__ y,
+                                   int relu, long long P, int C, const float* __restrict__ mean,
+                                   const float* __restrict__ invstd, float* __restrict__ dres,
+                                   double* __restrict__ part) {
+  const int chunk = blockIdx.y;
+  const long long rows = (P + BN_CHUNKS - 1) / BN_CHUNKS;
+  const long long r0 = chunk * rows, r1 = min(P, r0 + rows);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    double s0 = 0.0, s1 = 0.0;
+    if (MODE == 0) {
+      for (long long r = r0; r < r1; ++r) {
+        const double v = a[r * C + c];
+        s0 += v;
+        s1 += v * v;
+      }
+    } else {
+      const float m = mean[c], is = invstd[c];
+      for (long long r = r0; r < r1; ++r) {
+        float g = dy[r * C + c];
+        if (relu && !(y[r * C + c] > 0.f)) g = 0.f;
+        if (dres) dres[r * C + c] = g;
+        s0 += g;
+        s1 += (double)g * (double)((a[r * C + c] - m) * is);
+      }
+    }
+    part[(long long)chunk * 2 * C + c] = s0;
+    part[(long long)chunk * 2 * C + C + c] = s1;
+  }
+}
+
+__global__ void bn_stats_kernel(const double* __restrict__ part, long long P, int C, float eps, float momentum,
+                                float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean,
+                                float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < BN_CHUNKS; ++k) {
+    s0 += part[(long long)k * 2 * C + c];
+    s1 += part[(long long)k * 2 * C + C + c];
+  }
+  const double m = s0 / (double)P;
+  const double var = fmax(s1 / (double)P - m * m, 0.0);  // biased: used to normalise
+  mean[c] = (float)m;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    const double unb = P > 1 ? var * (double)P / (double)(P - 1) : var;  // unbiased: running estimate
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
+__global__ void bn_apply_kernel(const float* __restrict__ x, long long P, int C, const float* __restrict__ mean,
+                                const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, const float* __restrict__ res, int relu,
+                                float* __restrict__ y) {
+  const long long total = P * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float v = (x[i] - mean[c]) * invstd[c] * gamma[c] + beta[c];
+    if (res) v += res[i];
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = v;
+  }
+}
+
+__global__ void bn_grad_sums_kernel(const double* __restrict__ part, int C, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, double* __restrict__ sums) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < BN_CHUNKS; ++k) {
+    s0 += part[(long long)k * 2 * C + c];
+    s1 += part[(long long)k * 2 * C + C + c];
+  }
+  dbeta[c] = (float)s0;
+  dgamma[c] = (float)s1;
+  sums[c] = s0;
+  sums[C + c] = s1;
+}
+
+// dx = gamma * invstd * (g - sum(g) / P - xhat * sum(g * xhat) / P)
+__global__ void bn_dx_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu,
+                             const float* __restrict__ x, long long P, int C, const float* __restrict__ gamma,
+                             const float* __restrict__ mean, const float* __restrict__ invstd,
+                             const double* __restrict__ sums, float* __restrict__ dx) {
+  const long long total = P * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float g = dy[i];
+    if (relu && !(y[i] > 0.f)) g = 0.f;
+    const float xhat = (x[i] - mean[c]) * invstd[c];
+    const float mg = (float)(sums[c] / (double)P), mgx = (float)(sums[C + c] / (double)P);
+    dx[i] = gamma[c] * invstd[c] * (g - mg - xhat * mgx);
+  }
+}
+
+// 3x3 / 2, pad 1 (torchvision's maxpool); argmax = first maximum in (kh, kw) order, as torch CPU
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo,
+                                   float* __restrict__ y, int* __restrict__ idx) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long r = i / C;
+    const int ow = (int)(r % Wo);
+    const long long r2 = r / Wo;
+    const int oh = (int)(r2 % Ho), n = (int)(r2 / Ho);
+    float m = -INFINITY;
+    int arg = -1;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const float v = x[(((long long)n * H + ih) * W + iw) * C + c];
+        if (v > m || arg < 0) m = v, arg = ih * W + iw;
+      }
+    }
+    y[i] = m;
+    idx[i] = arg;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int* __restrict__ idx, int N, int H, int W,
+                                   int C, int Ho, int Wo, float* __restrict__ dx) {
+  const long long total = (long long)N * H * W * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long r = i / C;
+    const int iw = (int)(r % W);
+    const long long r2 = r / W;
+    const int ih = (int)(r2 % H), n = (int)(r2 / H);
+    const int me = ih * W + iw;
+    float s = 0.f;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int th = ih + 1 - kh;
+      if (th < 0 || (th & 1)) continue;
+      const int oh = th >> 1;
+      if (oh >= Ho) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tw = iw + 1 - kw;
+        if (tw < 0 || (tw & 1)) continue;
+        const int ow = tw >> 1;
+        if (ow >= Wo) continue;
+        const long long o = (((long long)n * Ho + oh) * Wo + ow) * C + c;
+        if (idx[o] == me) s += dy[o];
+      }
+    }
+    dx[i] = s;
+  }
+}
+
+// y[n][c] = mean over HW of x[n][hw][c] (sequential); backward dx = dy / HW
+__global__ void avgpool_fwd_kernel(const float* __restrict__ x, int N, int HW, int C, float* __restrict__ y) {
+  const long long total = (long long)N * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long n = i / C;
+    float s = 0.f;
+    for (int t = 0; t < HW; ++t) s += x[(n * HW + t) * C + c];
+    y[i] = s / (float)HW;
+  }
+}
+
+// dx[(n, t)][c] = dy[n][c] * scale (average pool over HW, or the clip mean over T frames)
+__global__ void broadcast_rows_kernel(const float* __restrict__ dy, int N, int T, int C, float scale,
+                                      float* __restrict__ dx) {
+  const long long total = (long long)N * T * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long n = i / ((long long)T * C);
+    dx[i] = dy[n * C + c] * scale;
+  }
+}
+
+// CrossEntropyLoss (mean over the batch): loss += (logsumexp - logit[label]) / B,
+// dlogits = (softmax - onehot) / B.  One block per row.
+__global__ void softmax_xent_kernel(const float* __restrict__ logits, const int* __restrict__ labels, int B, int C,
+                                    float* __restrict__ row_loss, float* __restrict__ dlogits) {
+  const int b = blockIdx.x;
+  const float* l = logits + (long long)b * C;
+  __shared__ float red[256];
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) m = fmaxf(m, l[c]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  m = red[0];
+  __syncthreads();
+  float se = 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) se += expf(l[c] - m);
+  red[threadIdx.x] = se;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  se = red[0];
+  const int lab = labels[b];
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    dlogits[(long long)b * C + c] = (expf(l[c] - m) / se - (c == lab ? 1.f : 0.f)) / (float)B;
+  if (threadIdx.x == 0) row_loss[b] = (logf(se) + m - l[lab]) / (float)B;
+}
+
+__global__ void sum_rows_kernel(const float* __restrict__ x, int rows, int C, float* __restrict__ y, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += x[(long long)r * C + c];
+  y[c] = accumulate ? y[c] + s : s;
+}
+
+__global__ void add_bias_kernel(float* __restrict__ y, int rows, int C, const float* __restrict__ b) {
+  const long long total = (long long)rows * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] += b[i % C];
+}
+
+// torch.optim.SGD (momentum, dampening 0, no weight decay): buf = g on the first step, else
+// momentum * buf + g; p -= lr * buf
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf, long long n,
+                           float lr, float momentum, int first) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float b = first ? g[i] : momentum * buf[i] + g[i];
+    buf[i] = b;
+    p[i] -= lr * b;
+  }
+}
+
+__global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, long long n, float alpha) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] += alpha * x[i];
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int HW, float* __restrict__ y) {
+  const long long total = (long long)N * C * HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long r = i / C;
+    const int t = (int)(r % HW);
+    const long long n = r / HW;
+    y[i] = x[(n * C + c) * HW + t];
+  }
+}
+
+// one rocBLAS handle per device (created on first use, never destroyed: lives with the process)
+rocblas_handle blas_handle(int dev) {
+  static std::mutex mu;
+  static rocblas_handle hs[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!hs[dev]) {
+    if (rocblas_create_handle(&hs[dev]) != rocblas_status_success) return hs[dev] = nullptr;
+    rocblas_set_atomics_mode(hs[dev], rocblas_atomics_not_allowed);
+  }
+  return hs[dev];
+}
+
+bool pos(long long v) { return v > 0; }
+}  // namespace
+}  // namespace eosv
+
+using namespace eosv;
+
+extern "C" {
+
+int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* d_a, int lda,
+               const float* d_b, int ldb, float beta, float* d_c, int ldc, eosv_stream_t stream) {
+  if (m < 0 || n < 0 || k < 0 || !d_c || (k > 0 && (!d_a || !d_b)) || lda <= 0 || ldb <= 0 || ldc < n)
+    return set_error("eosv_sgemm: bad argument"), EOSV_ERR_ARG;
+  if (m == 0 || n == 0) return EOSV_OK;
+  int dev = 0;
+  EOSV_HIP_CHECK(hipGetDevice(&dev));
+  rocblas_handle h = blas_handle(dev);
+  if (!h) return set_error("eosv_sgemm: rocblas_create_handle failed"), EOSV_ERR_HIP;
+  rocblas_set_stream(h, (hipStream_t)stream);
+  // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T on the same buffers
+  const rocblas_status st =
+      rocblas_sgemm(h, trans_b ? rocblas_operation_transpose : rocblas_operation_none,
+                    trans_a ? rocblas_operation_transpose : rocblas_operation_none, n, m, k, &alpha, d_b, ldb, d_a,
+                    lda, &beta, d_c, ldc);
+  if (st != rocblas_status_success)
+    return set_error(std::string("eosv_sgemm: ") + rocblas_status_to_string(st)), EOSV_ERR_HIP;
+  return EOSV_OK;
+}
+
+int eosv_im2col(const float* d_x, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_col,
+                eosv_stream_t stream) {
+  if (!d_x || !d_col || N <= 0 || H <= 0 || W <= 0 || C <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0)
+    return set_error("eosv_im2col: bad argument"), EOSV_ERR_ARG;
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return set_error("eosv_im2col: empty output"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for((long long)N * Ho * Wo * KH * KW * C)), dim3(256), 0,
+                     (hipStream_t)stream, d_x, N, H, W, C, KH, KW, stride, pad, Ho, Wo, d_col);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_col2im(const float* d_col, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_x,
+                eosv_stream_t stream) {
+  if (!d_x || !d_col || N <= 0 || H <= 0 || W <= 0 || C <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0)
+    return set_error("eosv_col2im: bad argument"), EOSV_ERR_ARG;
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return set_error("eosv_col2im: empty output"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
+                     d_col, N, H, W, C, KH, KW, stride, pad, Ho, Wo, d_x);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int64_t eosv_bn_workspace_bytes(int C) { return C > 0 ? (int64_t)(2 * BN_CHUNKS + 2) * C * 8 : 0; }
+
+int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gamma, const float* d_beta, float eps,
+                          float momentum, float* d_running_mean, float* d_running_var, const float* d_residual,
+                          int relu, float* d_y, float* d_save_mean, float* d_save_invstd, void* d_work,
+                          eosv_stream_t stream) {
+  if (!d_x || !d_y || !d_gamma || !d_beta || !d_save_mean || !d_save_invstd || !d_work || !pos(P) || C <= 0 ||
+      (!d_running_mean) != (!d_running_var) || !(eps > 0.f))
+    return set_error("eosv_bn_train_forward: bad argument"), EOSV_ERR_ARG;
+  const hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)d_work;
+  hipLaunchKernelGGL((bn_partials_kernel<0>), dim3((C + 255) / 256, BN_CHUNKS), dim3(256), 0, s, d_x, nullptr,
+                     nullptr, 0, (long long)P, C, nullptr, nullptr, nullptr, part);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, (long long)P, C, eps, momentum,
+                     d_running_mean, d_running_var, d_save_mean, d_save_invstd);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_x, (long long)P, C,
+                     d_save_mean, d_save_invstd, d_gamma, d_beta, d_residual, relu, d_y);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const float* d_x, int64_t P, int C,
+                           const float* d_gamma, const float* d_save_mean, const float* d_save_invstd, float* d_dx,
+                           float* d_dgamma, float* d_dbeta, float* d_dres, void* d_work, eosv_stream_t stream) {
+  if (!d_dy || !d_x || !d_gamma || !d_save_mean || !d_save_invstd || !d_dx || !d_dgamma || !d_dbeta || !d_work ||
+      !pos(P) || C <= 0 || (relu && !d_y))
+    return set_error("eosv_bn_train_backward: bad argument"), EOSV_ERR_ARG;
+  const hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)d_work;
+  double* sums = part + (long long)2 * BN_CHUNKS * C;
+  hipLaunchKernelGGL((bn_partials_kernel<1>), dim3((C + 255) / 256, BN_CHUNKS), dim3(256), 0, s, d_x, d_dy, d_y, relu,
+                     (long long)P, C, d_save_mean, d_save_invstd, d_dres, part);
+  hipLaunchKernelGGL(bn_grad_sums_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, C, d_dgamma, d_dbeta, sums);
+  hipLaunchKernelGGL(bn_dx_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_dy, d_y, relu, d_x,
+                     (long long)P, C, d_gamma, d_save_mean, d_save_invstd, sums, d_dx);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_maxpool_forward(const float* d_x, int N, int H, int W, int C, float* d_y, int32_t* d_idx,
+                         eosv_stream_t stream) {
+  if (!d_x || !d_y || !d_idx || N <= 0 || H <= 0 || W <= 0 || C <= 0)
+    return set_error("eosv_maxpool_forward: bad argument"), EOSV_ERR_ARG;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0,
+                     (hipStream_t)stream, d_x, N, H, W, C, Ho, Wo, d_y, d_idx);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_maxpool_backward(const float* d_dy, const int32_t* d_idx, int N, int H, int W, int C, float* d_dx,
+                          eosv_stream_t stream) {
+  if (!d_dy || !d_idx || !d_dx || N <= 0 || H <= 0 || W <= 0 || C <= 0)
+    return set_error("eosv_maxpool_backward: bad argument"), EOSV_ERR_ARG;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
+                     d_dy, d_idx, N, H, W, C, Ho, Wo, d_dx);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_avgpool_forward(const float* d_x, int N, int HW, int C, float* d_y, eosv_stream_t stream) {
+  if (!d_x || !d_y || N <= 0 || HW <= 0 || C <= 0) return set_error("eosv_avgpool_forward: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)N * C)), dim3(256), 0, (hipStream_t)stream, d_x, N,
+                     HW, C, d_y);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_broadcast_rows(const float* d_dy, int N, int T, int C, float scale, float* d_dx, eosv_stream_t stream) {
+  if (!d_dy || !d_dx || N <= 0 || T <= 0 || C <= 0) return set_error("eosv_broadcast_rows: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(broadcast_rows_kernel, dim3(grid_for((long long)N * T * C)), dim3(256), 0, (hipStream_t)stream,
+                     d_dy, N, T, C, scale, d_dx);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_softmax_xent(const float* d_logits, const int32_t* d_labels, int B, int C, float* d_row_loss,
+                      float* d_dlogits, eosv_stream_t stream) {
+  if (!d_logits || !d_labels || !d_row_loss || !d_dlogits || B <= 0 || C <= 0)
+    return set_error("eosv_softmax_xent: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, d_logits, d_labels, B, C,
+                     d_row_loss, d_dlogits);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_sum_rows(const float* d_x, int rows, int C, float* d_y, int accumulate, eosv_stream_t stream) {
+  if (!d_x || !d_y || rows <= 0 || C <= 0) return set_error("eosv_sum_rows: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_x, rows, C, d_y,
+                     accumulate);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_add_bias(float* d_y, int rows, int C, const float* d_bias, eosv_stream_t stream) {
+  if (!d_y || !d_bias || rows <= 0 || C <= 0) return set_error("eosv_add_bias: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(add_bias_kernel, dim3(grid_for((long long)rows * C)), dim3(256), 0, (hipStream_t)stream, d_y,
+                     rows, C, d_bias);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_sgd_momentum(float* d_p, const float* d_g, float* d_buf, int64_t n, float lr, float momentum, int first,
+                      eosv_stream_t stream) {
+  if (!d_p || !d_g || !d_buf || n <= 0) return set_error("eosv_sgd_momentum: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d_p, d_g, d_buf, (long long)n,
+                     lr, momentum, first);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_t stream) {
+  if (!d_y || !d_x || n <= 0) return set_error("eosv_axpy: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(axpy_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d_y, d_x, (long long)n, alpha);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_nchw_to_nhwc(const float* d_x, int N, int C, int H, int W, float* d_y, eosv_stream_t stream) {
+  if (!d_x || !d_y || N <= 0 || C <= 0 || H <= 0 || W <= 0)
+    return set_error("eosv_nchw_to_nhwc: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((long long)N * C * H * W)), dim3(256), 0, (hipStream_t)stream,
+                     d_x, N, C, H * W, d_y);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+}  // extern "C"

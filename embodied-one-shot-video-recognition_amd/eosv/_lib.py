@@ -25,7 +25,12 @@ _STATUS = {-1: "EOSV_ERR_ARG", -2: "EOSV_ERR_HIP", -3: "EOSV_ERR_OOM",
 EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_backbone_probe", "eosv_fc_forward",
            "eosv_clip_embed", "eosv_segment_mean", "eosv_match", "eosv_segment_match", "eosv_segment_match_episodes",
            "eosv_temporal_smooth", "eosv_normalize_frames", "eosv_crop_normalize_frames", "eosv_synth_frames", "eosv_plan_episodes", "eosv_profile_enable", "eosv_profile_read", "eosv_feature_dim", "eosv_device_bytes", "eosv_last_error",
-           "eosv_destroy")
+           "eosv_destroy",
+           # training path
+           "eosv_sgemm", "eosv_im2col", "eosv_col2im", "eosv_bn_workspace_bytes", "eosv_bn_train_forward",
+           "eosv_bn_train_backward", "eosv_maxpool_forward", "eosv_maxpool_backward", "eosv_avgpool_forward",
+           "eosv_broadcast_rows", "eosv_softmax_xent", "eosv_sum_rows", "eosv_add_bias", "eosv_sgd_momentum",
+           "eosv_axpy", "eosv_nchw_to_nhwc")
 
 
 class EosvDesc(ctypes.Structure):
@@ -73,6 +78,22 @@ def lib():
         "eosv_device_bytes": (i64, [vp]),
         "eosv_last_error": (ctypes.c_char_p, []),
         "eosv_destroy": (None, [vp]),
+        "eosv_sgemm": (i32, [i32, i32, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, vp]),
+        "eosv_im2col": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+        "eosv_col2im": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+        "eosv_bn_workspace_bytes": (i64, [i32]),
+        "eosv_bn_train_forward": (i32, [vp, i64, i32, vp, vp, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp]),
+        "eosv_bn_train_backward": (i32, [vp, vp, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "eosv_maxpool_forward": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
+        "eosv_maxpool_backward": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+        "eosv_avgpool_forward": (i32, [vp, i32, i32, i32, vp, vp]),
+        "eosv_broadcast_rows": (i32, [vp, i32, i32, i32, f32, vp, vp]),
+        "eosv_softmax_xent": (i32, [vp, vp, i32, i32, vp, vp, vp]),
+        "eosv_sum_rows": (i32, [vp, i32, i32, vp, i32, vp]),
+        "eosv_add_bias": (i32, [vp, i32, i32, vp, vp]),
+        "eosv_sgd_momentum": (i32, [vp, vp, vp, i64, f32, f32, i32, vp]),
+        "eosv_axpy": (i32, [vp, vp, i64, f32, vp]),
+        "eosv_nchw_to_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

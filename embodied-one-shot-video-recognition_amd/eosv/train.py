@@ -1,0 +1,353 @@
+"""Native training step for TrainNetwork.finetune_model.
+
+Restates one iteration of the reference's loop (network_train.py:86-116) on the device:
+
+    feature, output = model(video)                  # ResNet in train mode: batch-statistics BN
+    feature = feature.view(b, T, -1).mean(dim=1)    # :100, :110
+    output = model.fc(feature); loss = CrossEntropyLoss()(output, label)
+    loss.backward(); optimizer_1.step(); optimizer_2.step()   # SGD(momentum=0.9): convnet / fc
+
+with the f32 kernels of csrc/train.hip behind the C ABI (eosv_sgemm, eosv_im2col,
+eosv_bn_train_forward, ...).  PyTorch only provides the device buffers; every arithmetic step
+is a library call, and there is no CPU path.  Layouts: activations NHWC ([P][C] rows), conv
+weights [Cout][KH][KW][Cin] (the state_dict's [Cout][Cin][KH][KW] permuted at load / export).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import arch as _arch
+from ._lib import check, lib, ptr, stream_ptr
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+def _f(t):
+    return ptr(t)
+
+
+@dataclass
+class _Conv:
+    name: str
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+    w: torch.Tensor = None      # [Cout][K] with K = (kh, kw, cin)
+    g: torch.Tensor = None
+    buf: torch.Tensor = None
+
+    @property
+    def K(self):
+        return self.k * self.k * self.cin
+
+
+@dataclass
+class _BN:
+    name: str
+    c: int
+    gamma: torch.Tensor = None
+    beta: torch.Tensor = None
+    rm: torch.Tensor = None
+    rv: torch.Tensor = None
+    nbt: int = 0
+    dgamma: torch.Tensor = None
+    dbeta: torch.Tensor = None
+    buf_g: torch.Tensor = None
+    buf_b: torch.Tensor = None
+
+
+@dataclass
+class _Block:
+    convs: List[_Conv]
+    bns: List[_BN]
+    ds: Optional[_Conv] = None
+    ds_bn: Optional[_BN] = None
+    saved: Dict[str, object] = field(default_factory=dict)
+
+
+class NativeTrainer:
+    """ResNet-18/50 + fc trained with the reference's recipe (network_train.py:75-79)."""
+
+    def __init__(self, arch: str = "resnet50", num_classes: int = 64, device: int = 0):
+        self.spec = _arch.SPECS[arch]
+        self.num_classes = num_classes
+        self.dev = torch.device("cuda", device)
+        self.L = lib()
+        self.stem = _Conv("convnet.0", 3, 64, 7, 2, 3)
+        self.stem_bn = _BN("convnet.1", 64)
+        self.blocks: List[_Block] = []
+        inplanes = 64
+        for li, (planes, n) in enumerate(zip((64, 128, 256, 512), self.spec.layers)):
+            for bi in range(n):
+                stride = 2 if (li > 0 and bi == 0) else 1
+                p = f"convnet.{4 + li}.{bi}"
+                if self.spec.block == "basic":
+                    convs = [_Conv(p + ".conv1", inplanes, planes, 3, stride, 1),
+                             _Conv(p + ".conv2", planes, planes, 3, 1, 1)]
+                    bns = [_BN(p + ".bn1", planes), _BN(p + ".bn2", planes)]
+                else:
+                    convs = [_Conv(p + ".conv1", inplanes, planes, 1, 1, 0),
+                             _Conv(p + ".conv2", planes, planes, 3, stride, 1),
+                             _Conv(p + ".conv3", planes, planes * 4, 1, 1, 0)]
+                    bns = [_BN(p + ".bn1", planes), _BN(p + ".bn2", planes), _BN(p + ".bn3", planes * 4)]
+                cout = planes * self.spec.expansion
+                blk = _Block(convs, bns)
+                if bi == 0 and (stride != 1 or inplanes != cout):
+                    blk.ds = _Conv(p + ".downsample.0", inplanes, cout, 1, stride, 0)
+                    blk.ds_bn = _BN(p + ".downsample.1", cout)
+                self.blocks.append(blk)
+                inplanes = cout
+        self.D = inplanes
+        self.fc_w = self.fc_b = None
+        self.step_count = 0
+        self._scratch: Dict[str, torch.Tensor] = {}
+        self.work = torch.empty(int(self.L.eosv_bn_workspace_bytes(2048)) // 4 + 4, dtype=torch.float32,
+                                device=self.dev)
+
+    # ------------------------------------------------------------------ parameters
+    def _convs(self):
+        yield self.stem
+        for b in self.blocks:
+            yield from b.convs
+            if b.ds is not None:
+                yield b.ds
+
+    def _bns(self):
+        yield self.stem_bn
+        for b in self.blocks:
+            yield from b.bns
+            if b.ds_bn is not None:
+                yield b.ds_bn
+
+    def load_state_dict(self, sd: Dict[str, object]):
+        """The reference model's state_dict (numpy arrays or tensors, any device)."""
+        def t(name):
+            v = sd[name]
+            v = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+            return v.detach().to(self.dev, torch.float32).contiguous()
+
+        for c in self._convs():
+            w = t(c.name + ".weight")                       # [Cout][Cin][KH][KW]
+            c.w = w.permute(0, 2, 3, 1).reshape(c.cout, c.K).contiguous()
+            c.g = torch.zeros_like(c.w)
+            c.buf = torch.zeros_like(c.w)
+        for b in self._bns():
+            b.gamma, b.beta = t(b.name + ".weight"), t(b.name + ".bias")
+            b.rm, b.rv = t(b.name + ".running_mean"), t(b.name + ".running_var")
+            nbt = sd.get(b.name + ".num_batches_tracked", 0)
+            b.nbt = int(nbt.item() if isinstance(nbt, torch.Tensor) else np.asarray(nbt))
+            b.dgamma, b.dbeta = torch.zeros_like(b.gamma), torch.zeros_like(b.beta)
+            b.buf_g, b.buf_b = torch.zeros_like(b.gamma), torch.zeros_like(b.beta)
+        self.fc_w, self.fc_b = t("fc.weight"), t("fc.bias")
+        self.fc_gw, self.fc_gb = torch.zeros_like(self.fc_w), torch.zeros_like(self.fc_b)
+        self.fc_bw, self.fc_bb = torch.zeros_like(self.fc_w), torch.zeros_like(self.fc_b)
+        self.step_count = 0
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """The reference's state_dict layout, on the CPU (torch.save, network_train.py:131)."""
+        out = {}
+        for c in self._convs():
+            out[c.name + ".weight"] = c.w.view(c.cout, c.k, c.k, c.cin).permute(0, 3, 1, 2).contiguous().cpu()
+        for b in self._bns():
+            out[b.name + ".weight"] = b.gamma.cpu()
+            out[b.name + ".bias"] = b.beta.cpu()
+            out[b.name + ".running_mean"] = b.rm.cpu()
+            out[b.name + ".running_var"] = b.rv.cpu()
+            out[b.name + ".num_batches_tracked"] = torch.tensor(b.nbt, dtype=torch.int64)
+        out["fc.weight"] = self.fc_w.cpu()
+        out["fc.bias"] = self.fc_b.cpu()
+        return out
+
+    # ------------------------------------------------------------------ building blocks
+    def _buf(self, key, n):
+        t = self._scratch.get(key)
+        if t is None or t.numel() < n:
+            t = torch.empty(n, dtype=torch.float32, device=self.dev)
+            self._scratch[key] = t
+        return t[:n]
+
+    def _conv_fwd(self, x, shape, c: _Conv, s):
+        N, H, W, _ = shape
+        Ho, Wo = (H + 2 * c.pad - c.k) // c.stride + 1, (W + 2 * c.pad - c.k) // c.stride + 1
+        P = N * Ho * Wo
+        if c.k == 1 and c.stride == 1:
+            col = x
+        else:
+            col = self._buf("col", P * c.K)
+            check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
+        y = torch.empty(P * c.cout, dtype=torch.float32, device=self.dev)
+        check(self.L.eosv_sgemm(0, 1, P, c.cout, c.K, 1.0, _f(col), c.K, _f(c.w), c.K, 0.0, _f(y), c.cout, s),
+              "eosv_sgemm")
+        return y, (N, Ho, Wo, c.cout)
+
+    def _conv_bwd(self, dz, x, shape, c: _Conv, s, need_dx=True):
+        """dW = dz^T . col(x); returns dx = col2im(dz . W) (NHWC, shape of x) when need_dx."""
+        N, H, W, _ = shape
+        Ho, Wo = (H + 2 * c.pad - c.k) // c.stride + 1, (W + 2 * c.pad - c.k) // c.stride + 1
+        P = N * Ho * Wo
+        direct = c.k == 1 and c.stride == 1
+        if direct:
+            col = x
+        else:
+            col = self._buf("col", P * c.K)
+            check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
+        check(self.L.eosv_sgemm(1, 0, c.cout, c.K, P, 1.0, _f(dz), c.cout, _f(col), c.K, 0.0, _f(c.g), c.K, s),
+              "eosv_sgemm")
+        if not need_dx:
+            return None
+        dx = torch.empty(N * H * W * c.cin, dtype=torch.float32, device=self.dev)
+        dcol = dx if direct else self._buf("dcol", P * c.K)
+        check(self.L.eosv_sgemm(0, 0, P, c.K, c.cout, 1.0, _f(dz), c.cout, _f(c.w), c.K, 0.0, _f(dcol), c.K, s),
+              "eosv_sgemm")
+        if not direct:
+            check(self.L.eosv_col2im(_f(dcol), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(dx), s), "eosv_col2im")
+        return dx
+
+    def _bn_fwd(self, z, P, b: _BN, relu, res, s):
+        y = torch.empty_like(z)
+        mean = torch.empty(b.c, dtype=torch.float32, device=self.dev)
+        invstd = torch.empty_like(mean)
+        check(self.L.eosv_bn_train_forward(_f(z), P, b.c, _f(b.gamma), _f(b.beta), BN_EPS, BN_MOMENTUM, _f(b.rm),
+                                           _f(b.rv), _f(res), int(relu), _f(y), _f(mean), _f(invstd), _f(self.work),
+                                           s), "eosv_bn_train_forward")
+        b.nbt += 1
+        return y, (mean, invstd)
+
+    def _bn_bwd(self, dy, y, relu, z, P, b: _BN, stats, s, want_dres=False):
+        dz = torch.empty_like(z)
+        dres = torch.empty_like(z) if want_dres else None
+        check(self.L.eosv_bn_train_backward(_f(dy), _f(y), int(relu), _f(z), P, b.c, _f(b.gamma), _f(stats[0]),
+                                            _f(stats[1]), _f(dz), _f(b.dgamma), _f(b.dbeta), _f(dres),
+                                            _f(self.work), s), "eosv_bn_train_backward")
+        return dz, dres
+
+    # ------------------------------------------------------------------ one iteration
+    def step(self, frames: torch.Tensor, labels, T: int, lr_conv: float, lr_fc: float, momentum: float = 0.9):
+        """frames [B*T, 3, H, W] f32 (clip-major, as video.view(-1, 3, H, W)), labels [B] ints.
+        Runs forward, loss, backward and both SGD updates; returns (loss, logits [B, C])."""
+        if self.fc_w is None:
+            raise RuntimeError("NativeTrainer.step: load_state_dict first")
+        frames = frames.to(self.dev, torch.float32).contiguous()
+        NT, _, H, W = frames.shape
+        if NT % T:
+            raise ValueError("frames must be B*T clip-major rows")
+        B = NT // T
+        lab = torch.as_tensor(np.asarray(labels, np.int32).reshape(-1), device=self.dev)
+        if lab.numel() != B:
+            raise ValueError("one label per clip")
+        s = stream_ptr()
+        L = self.L
+        # ---- forward
+        x0 = torch.empty(NT * H * W * 3, dtype=torch.float32, device=self.dev)
+        check(L.eosv_nchw_to_nhwc(_f(frames), NT, 3, H, W, _f(x0), s), "eosv_nchw_to_nhwc")
+        shp0 = (NT, H, W, 3)
+        z0, shp1 = self._conv_fwd(x0, shp0, self.stem, s)
+        P1 = shp1[0] * shp1[1] * shp1[2]
+        a0, st0 = self._bn_fwd(z0, P1, self.stem_bn, True, None, s)
+        Hq, Wq = (shp1[1] - 1) // 2 + 1, (shp1[2] - 1) // 2 + 1
+        h = torch.empty(NT * Hq * Wq * 64, dtype=torch.float32, device=self.dev)
+        idx = torch.empty(NT * Hq * Wq * 64, dtype=torch.int32, device=self.dev)
+        check(L.eosv_maxpool_forward(_f(a0), shp1[0], shp1[1], shp1[2], 64, _f(h), _f(idx), s), "eosv_maxpool_forward")
+        shp = (NT, Hq, Wq, 64)
+        for blk in self.blocks:
+            sv = blk.saved = {"x": h, "shape": shp, "z": [], "y": [], "st": [], "in": [], "inshape": []}
+            cur, cshp = h, shp
+            nl = len(blk.convs)
+            if blk.ds is not None:
+                zd, dshp = self._conv_fwd(h, shp, blk.ds, s)
+                Pd = dshp[0] * dshp[1] * dshp[2]
+                sc, std = self._bn_fwd(zd, Pd, blk.ds_bn, False, None, s)
+                sv["ds"] = (zd, sc, std, Pd)
+            else:
+                sc = h
+            for i, (c, b) in enumerate(zip(blk.convs, blk.bns)):
+                z, oshp = self._conv_fwd(cur, cshp, c, s)
+                P = oshp[0] * oshp[1] * oshp[2]
+                last = i == nl - 1
+                y, st = self._bn_fwd(z, P, b, True, sc if last else None, s)
+                sv["in"].append(cur)
+                sv["inshape"].append(cshp)
+                sv["z"].append(z)
+                sv["y"].append(y)
+                sv["st"].append((st, P))
+                cur, cshp = y, oshp
+            h, shp = cur, cshp
+        N4, H4, W4, D = shp
+        feat = torch.empty(N4 * D, dtype=torch.float32, device=self.dev)
+        check(L.eosv_avgpool_forward(_f(h), N4, H4 * W4, D, _f(feat), s), "eosv_avgpool_forward")
+        fm = torch.empty(B * D, dtype=torch.float32, device=self.dev)
+        check(L.eosv_avgpool_forward(_f(feat), B, T, D, _f(fm), s), "eosv_avgpool_forward")  # mean over the T frames
+        C = self.num_classes
+        logits = torch.empty(B * C, dtype=torch.float32, device=self.dev)
+        check(L.eosv_sgemm(0, 1, B, C, D, 1.0, _f(fm), D, _f(self.fc_w), D, 0.0, _f(logits), C, s), "eosv_sgemm")
+        check(L.eosv_add_bias(_f(logits), B, C, _f(self.fc_b), s), "eosv_add_bias")
+        row_loss = torch.empty(B, dtype=torch.float32, device=self.dev)
+        dlog = torch.empty(B * C, dtype=torch.float32, device=self.dev)
+        check(L.eosv_softmax_xent(_f(logits), _f(lab), B, C, _f(row_loss), _f(dlog), s), "eosv_softmax_xent")
+        # ---- backward
+        check(L.eosv_sgemm(1, 0, C, D, B, 1.0, _f(dlog), C, _f(fm), D, 0.0, _f(self.fc_gw), D, s), "eosv_sgemm")
+        check(L.eosv_sum_rows(_f(dlog), B, C, _f(self.fc_gb), 0, s), "eosv_sum_rows")
+        dfm = torch.empty(B * D, dtype=torch.float32, device=self.dev)
+        check(L.eosv_sgemm(0, 0, B, D, C, 1.0, _f(dlog), C, _f(self.fc_w), D, 0.0, _f(dfm), D, s), "eosv_sgemm")
+        dfeat = torch.empty(N4 * D, dtype=torch.float32, device=self.dev)
+        check(L.eosv_broadcast_rows(_f(dfm), B, T, D, 1.0 / T, _f(dfeat), s), "eosv_broadcast_rows")
+        dh = torch.empty(N4 * H4 * W4 * D, dtype=torch.float32, device=self.dev)
+        check(L.eosv_broadcast_rows(_f(dfeat), N4, H4 * W4, D, 1.0 / (H4 * W4), _f(dh), s), "eosv_broadcast_rows")
+        for blk in reversed(self.blocks):
+            sv = blk.saved
+            nl = len(blk.convs)
+            dres = None
+            g = dh
+            for i in reversed(range(nl)):
+                c, b = blk.convs[i], blk.bns[i]
+                st, P = sv["st"][i]
+                dz, dr = self._bn_bwd(g, sv["y"][i], True, sv["z"][i], P, b, st, s, want_dres=(i == nl - 1))
+                if i == nl - 1:
+                    dres = dr
+                g = self._conv_bwd(dz, sv["in"][i], sv["inshape"][i], c, s, need_dx=True)
+            if blk.ds is not None:
+                zd, sc, std, Pd = sv["ds"]
+                dzd, _ = self._bn_bwd(dres, None, False, zd, Pd, blk.ds_bn, std, s)
+                gd = self._conv_bwd(dzd, sv["x"], sv["shape"], blk.ds, s, need_dx=True)
+                check(L.eosv_axpy(_f(g), _f(gd), g.numel(), 1.0, s), "eosv_axpy")
+            else:
+                check(L.eosv_axpy(_f(g), _f(dres), g.numel(), 1.0, s), "eosv_axpy")
+            dh = g
+            blk.saved = {}
+        da0 = torch.empty(P1 * 64, dtype=torch.float32, device=self.dev)
+        check(L.eosv_maxpool_backward(_f(dh), _f(idx), shp1[0], shp1[1], shp1[2], 64, _f(da0), s),
+              "eosv_maxpool_backward")
+        dz0, _ = self._bn_bwd(da0, a0, True, z0, P1, self.stem_bn, st0, s)
+        self._conv_bwd(dz0, x0, shp0, self.stem, s, need_dx=False)
+        # ---- SGD (optimizer_1: convnet, optimizer_2: fc; first step initialises the momentum)
+        first = int(self.step_count == 0)
+        for c in self._convs():
+            check(L.eosv_sgd_momentum(_f(c.w), _f(c.g), _f(c.buf), c.w.numel(), lr_conv, momentum, first, s), "sgd")
+        for b in self._bns():
+            check(L.eosv_sgd_momentum(_f(b.gamma), _f(b.dgamma), _f(b.buf_g), b.c, lr_conv, momentum, first, s), "sgd")
+            check(L.eosv_sgd_momentum(_f(b.beta), _f(b.dbeta), _f(b.buf_b), b.c, lr_conv, momentum, first, s), "sgd")
+        check(L.eosv_sgd_momentum(_f(self.fc_w), _f(self.fc_gw), _f(self.fc_bw), self.fc_w.numel(), lr_fc, momentum,
+                                  first, s), "sgd")
+        check(L.eosv_sgd_momentum(_f(self.fc_b), _f(self.fc_gb), _f(self.fc_bb), self.fc_b.numel(), lr_fc, momentum,
+                                  first, s), "sgd")
+        self.step_count += 1
+        return float(row_loss.sum().item()), logits.view(B, C)
+
+    def grads(self) -> Dict[str, torch.Tensor]:
+        """The last step's gradients in the state_dict layout (CPU), for parity checks."""
+        out = {}
+        for c in self._convs():
+            out[c.name + ".weight"] = c.g.view(c.cout, c.k, c.k, c.cin).permute(0, 3, 1, 2).contiguous().cpu()
+        for b in self._bns():
+            out[b.name + ".weight"] = b.dgamma.cpu()
+            out[b.name + ".bias"] = b.dbeta.cpu()
+        out["fc.weight"] = self.fc_gw.cpu()
+        out["fc.bias"] = self.fc_gb.cpu()
+        return out

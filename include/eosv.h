@@ -178,6 +178,60 @@ int eosv_plan_episodes(const int32_t* class_sizes, int n_classes, int n_way, int
 int eosv_backbone_probe(eosv_handle* h, const float* d_frames, int B, int stage, float* d_out,
                         eosv_stream_t stream);
 
+/* ---- Training path (reference network_train.py:52-131, epoch_dataloader.py) ----
+ * TrainNetwork.finetune_model: ResNet-18/50 in train mode (batch-statistics BN), fc +
+ * CrossEntropyLoss, loss.backward(), torch.optim.SGD(momentum 0.9) on convnet and fc.  The
+ * Python trainer (eosv/train.py) chains these f32 kernels; activations NHWC ([P][C] rows),
+ * conv weights [Cout][KH][KW][Cin].  No handle: every call is stateless on caller buffers. */
+
+/* Row-major C[m][n] = alpha * op(A) op(B) + beta * C (op = transpose when trans_*), rocBLAS
+ * sgemm with atomics disabled (deterministic).  The conv GEMMs of a training step: forward
+ * Y = Xcol W^T (models.py:19 in train mode), input gradient dXcol = dY W and weight gradient
+ * dW = dY^T Xcol (loss.backward(), network_train.py:114). */
+int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* d_a, int lda,
+               const float* d_b, int ldb, float beta, float* d_c, int ldc, eosv_stream_t stream);
+/* im2col of NHWC x: col[(n, oh, ow)][(kh, kw, c)], zero padding; col2im is its adjoint
+ * (gather-sum, overwrites d_x). */
+int eosv_im2col(const float* d_x, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_col,
+                eosv_stream_t stream);
+int eosv_col2im(const float* d_col, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_x,
+                eosv_stream_t stream);
+/* Batch norm in train mode (nn.BatchNorm2d.train(), eps, momentum): batch mean / biased variance
+ * normalise, the running estimates take the unbiased variance; y = bn(x) (+ residual) (ReLU).
+ * Saves mean and 1/sqrt(var + eps) for the backward.  d_work: eosv_bn_workspace_bytes(C). */
+int64_t eosv_bn_workspace_bytes(int C);
+int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gamma, const float* d_beta, float eps,
+                          float momentum, float* d_running_mean, float* d_running_var, const float* d_residual,
+                          int relu, float* d_y, float* d_save_mean, float* d_save_invstd, void* d_work,
+                          eosv_stream_t stream);
+/* Its backward from dy = dL/dy (masked by y > 0 when relu): dx, dgamma, dbeta; d_dres (optional)
+ * receives the masked dy, the gradient of the residual branch. */
+int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const float* d_x, int64_t P, int C,
+                           const float* d_gamma, const float* d_save_mean, const float* d_save_invstd, float* d_dx,
+                           float* d_dgamma, float* d_dbeta, float* d_dres, void* d_work, eosv_stream_t stream);
+/* Max pool 3x3 / 2, pad 1 with argmax indices (first maximum in window order, as torch CPU);
+ * backward gathers dy into the argmax positions. */
+int eosv_maxpool_forward(const float* d_x, int N, int H, int W, int C, float* d_y, int32_t* d_idx,
+                         eosv_stream_t stream);
+int eosv_maxpool_backward(const float* d_dy, const int32_t* d_idx, int N, int H, int W, int C, float* d_dx,
+                          eosv_stream_t stream);
+/* Average pool over HW ([N][HW][C] -> [N][C]); dx[(n, t)][c] = dy[n][c] * scale (its backward
+ * with scale 1/HW, and the clip mean's over T frames, network_train.py:110). */
+int eosv_avgpool_forward(const float* d_x, int N, int HW, int C, float* d_y, eosv_stream_t stream);
+int eosv_broadcast_rows(const float* d_dy, int N, int T, int C, float scale, float* d_dx, eosv_stream_t stream);
+/* nn.CrossEntropyLoss (mean): per-row loss terms (sum = loss) and dL/dlogits. */
+int eosv_softmax_xent(const float* d_logits, const int32_t* d_labels, int B, int C, float* d_row_loss,
+                      float* d_dlogits, eosv_stream_t stream);
+/* y[c] (+)= sum over rows of x[r][c]; y[r][c] += bias[c]. */
+int eosv_sum_rows(const float* d_x, int rows, int C, float* d_y, int accumulate, eosv_stream_t stream);
+int eosv_add_bias(float* d_y, int rows, int C, const float* d_bias, eosv_stream_t stream);
+/* torch.optim.SGD step (momentum, dampening 0): buf = first ? g : momentum buf + g; p -= lr buf. */
+int eosv_sgd_momentum(float* d_p, const float* d_g, float* d_buf, int64_t n, float lr, float momentum, int first,
+                      eosv_stream_t stream);
+/* y += alpha x; NCHW -> NHWC. */
+int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_t stream);
+int eosv_nchw_to_nhwc(const float* d_x, int N, int C, int H, int W, float* d_y, eosv_stream_t stream);
+
 /* Feature dimension D of the handle's backbone. */
 int eosv_feature_dim(const eosv_handle* h);
 

@@ -1,0 +1,227 @@
+"""GPU: the native training step (eosv/train.py) against the reference's
+recipe run by torch on the CPU (network_train.py:75-116: model.train(), clip mean over T frames,
+fc, CrossEntropyLoss, backward, SGD(momentum=0.9) for convnet and fc).
+
+The oracle is the torch.nn restatement of the reference model (oracle/resnet_ref.py, the same
+module the inference parity uses) with torch's own autograd and optimiser, run twice: in f64
+(the reference values) and in f32 (the yardstick: what torch's own f32 arithmetic gets).  Both
+sides start from the same synthetic state_dict and see the same frames and labels for two
+iterations (the second exercises the momentum buffers).
+
+A small batch (8 frames of 96x96, 3x3 maps and 72 BN samples per channel at layer4) makes the
+backward ill-conditioned: ResNet-50's gradients below layer4 move by ~4e-3 between torch f32
+and f64, and a ReLU whose pre-activation sits within rounding of 0 can flip its mask between
+two f32 forwards, which moves a cancelling BN gradient sum by ~1e-2 relative (measured: ResNet-50
+layer4.2.bn2).  Bounds: the first loss within 1e-4 relative of f64; the second loss within
+max(4 x torch-f32's distance, 1e-4 relative); every gradient of the first step within
+max(4 x torch-f32's distance, 2e-2 relative) of f64 (a wrong kernel is off by O(1)); every
+parameter / BN running statistic after two steps within max(4 x torch-f32's distance, 1e-5
+relative), tensors compared by norm.
+"""
+import numpy as np
+import pytest
+import torch
+
+from eosv import arch, synth
+from eosv.train import NativeTrainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(name, sd, frames, labels, T, lr1, lr2, steps, dtype):
+    from oracle.resnet_ref import ModelResNetRef
+
+    m = ModelResNetRef(name, 64)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.to(dtype).train()
+    o1 = torch.optim.SGD(m.convnet.parameters(), lr=lr1, momentum=0.9)
+    o2 = torch.optim.SGD(m.fc.parameters(), lr=lr2, momentum=0.9)
+    crit = torch.nn.CrossEntropyLoss()
+    B = frames.shape[0] // T
+    losses, grads0 = [], None
+    for it in range(steps):
+        o1.zero_grad()
+        o2.zero_grad()
+        feature, _ = m(frames.to(dtype))
+        feature = feature.view(B, T, -1).mean(dim=1)
+        out = m.fc(feature)
+        loss = crit(out, torch.as_tensor(labels, dtype=torch.long))
+        loss.backward()
+        if it == 0:
+            grads0 = {k: p.grad.detach().double().clone() for k, p in m.named_parameters()}
+        o1.step()
+        o2.step()
+        losses.append(float(loss.detach()))
+    return losses, grads0, m.state_dict()
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_train_step_matches_torch_reference(name):
+    torch.manual_seed(0)
+    T, B, H = 4, 2, 96
+    frames = torch.randn(B * T, 3, H, H)
+    labels = [3, 17]
+    lr1, lr2 = 1e-3, 1e-2  # 10x the reference's (network_train.py:140)
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    ref_losses, ref_g, ref_sd = _oracle(name, sd, frames, labels, T, lr1, lr2, 2, torch.float64)
+    f32_losses, f32_g, f32_sd = _oracle(name, sd, frames, labels, T, lr1, lr2, 2, torch.float32)
+
+    tr = NativeTrainer(name, 64, device=0)
+    tr.load_state_dict(sd)
+    l0, logits = tr.step(frames.cuda(), labels, T, lr1, lr2)
+    g0 = tr.grads()
+    l1, _ = tr.step(frames.cuda(), labels, T, lr1, lr2)
+    print(f"[{name}] loss {l0:.6f} / {ref_losses[0]:.6f}, {l1:.6f} / {ref_losses[1]:.6f}")
+    assert abs(l0 - ref_losses[0]) <= 1e-4 * abs(ref_losses[0])
+    # the second loss inherits the first step's gradient conditioning: same yardstick
+    assert abs(l1 - ref_losses[1]) <= max(4 * abs(f32_losses[1] - ref_losses[1]), 1e-4 * abs(ref_losses[1]))
+    worst = 0.0
+    for k, gr in ref_g.items():
+        norm = max(float(gr.norm()), 1e-12)
+        err = float((g0[k].double() - gr).norm()) / norm
+        yard = float((f32_g[k] - gr).norm()) / norm
+        worst = max(worst, err)
+        assert err <= max(4 * yard, 2e-2), (k, err, yard)
+    print(f"[{name}] worst relative gradient error {worst:.2e}")
+    got = tr.state_dict()
+    for k, v in ref_sd.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(v), k
+            continue
+        v = v.double()
+        err = float((got[k].double() - v).norm())
+        yard = float((f32_sd[k].double() - v).norm())
+        assert err <= max(4 * yard, 1e-6 * v.numel() ** 0.5 + 1e-5 * float(v.norm())), (k, err, yard)
+
+
+def test_train_kernels_reject_bad_arguments():
+    from eosv._lib import EosvError, check, lib
+
+    L = lib()
+    x = torch.zeros(16, device="cuda")
+    with pytest.raises(EosvError):
+        check(L.eosv_im2col(x.data_ptr(), 1, 2, 2, 1, 3, 3, 0, 1, x.data_ptr(), None), "eosv_im2col")
+    with pytest.raises(EosvError):
+        check(L.eosv_sgemm(0, 0, 2, 2, 2, 1.0, 0, 2, x.data_ptr(), 2, 0.0, x.data_ptr(), 2, None), "eosv_sgemm")
+    with pytest.raises(EosvError):
+        check(L.eosv_bn_train_forward(x.data_ptr(), 0, 4, x.data_ptr(), x.data_ptr(), 1e-5, 0.1, 0, 0, 0, 1,
+                                      x.data_ptr(), x.data_ptr(), x.data_ptr(), x.data_ptr(), None),
+              "eosv_bn_train_forward")
+
+
+def _call(fn, *args):
+    from eosv._lib import check, stream_ptr
+
+    check(fn(*args, stream_ptr()), fn.__name__)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("k,stride,pad,cin,cout", [(3, 1, 1, 8, 16), (3, 2, 1, 8, 16), (1, 2, 0, 16, 8), (7, 2, 3, 3, 8)])
+def test_conv_forward_and_gradients_vs_torch(k, stride, pad, cin, cout):
+    """im2col + eosv_sgemm forward, weight gradient and col2im input gradient against torch
+    autograd in f64 on well-conditioned random data (no BN, no ReLU): 1e-5 relative."""
+    from eosv._lib import lib
+
+    L = lib()
+    torch.manual_seed(1)
+    N, H, W = 2, 9, 11
+    x = torch.randn(N, cin, H, W, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, k, k, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, stride=stride, padding=pad)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    Ho, Wo = y.shape[2], y.shape[3]
+    P, K = N * Ho * Wo, k * k * cin
+    xd = x.detach().permute(0, 2, 3, 1).contiguous().float().cuda()
+    wd = w.detach().permute(0, 2, 3, 1).reshape(cout, K).contiguous().float().cuda()
+    dyd = dy.permute(0, 2, 3, 1).reshape(P, cout).contiguous().float().cuda()
+    col = torch.empty(P * K, device="cuda")
+    _call(L.eosv_im2col, xd.data_ptr(), N, H, W, cin, k, k, stride, pad, col.data_ptr())
+    yd = torch.empty(P * cout, device="cuda")
+    _call(L.eosv_sgemm, 0, 1, P, cout, K, 1.0, col.data_ptr(), K, wd.data_ptr(), K, 0.0, yd.data_ptr(), cout)
+    gw = torch.empty(cout * K, device="cuda")
+    _call(L.eosv_sgemm, 1, 0, cout, K, P, 1.0, dyd.data_ptr(), cout, col.data_ptr(), K, 0.0, gw.data_ptr(), K)
+    dcol = torch.empty(P * K, device="cuda")
+    _call(L.eosv_sgemm, 0, 0, P, K, cout, 1.0, dyd.data_ptr(), cout, wd.data_ptr(), K, 0.0, dcol.data_ptr(), K)
+    gx = torch.empty(N * H * W * cin, device="cuda")
+    _call(L.eosv_col2im, dcol.data_ptr(), N, H, W, cin, k, k, stride, pad, gx.data_ptr())
+
+    def rel(a, b):
+        return float((a.double().cpu() - b).norm() / b.norm())
+
+    assert rel(yd.view(N, Ho, Wo, cout).permute(0, 3, 1, 2), y.detach()) < 1e-5
+    assert rel(gw.view(cout, k, k, cin).permute(0, 3, 1, 2), w.grad) < 1e-5
+    assert rel(gx.view(N, H, W, cin).permute(0, 3, 1, 2), x.grad) < 1e-5
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
+def test_batchnorm_train_forward_backward_vs_torch(relu, res):
+    """eosv_bn_train_forward / _backward against nn.BatchNorm2d in train mode (f64 autograd):
+    output, saved statistics, running estimates, dx, dgamma, dbeta, residual gradient."""
+    from eosv._lib import lib
+
+    L = lib()
+    torch.manual_seed(2)
+    N, C, H, W = 3, 40, 5, 7
+    P = N * H * W
+    x = torch.randn(N, C, H, W, dtype=torch.float64, requires_grad=True) * 2 + 0.5
+    x.retain_grad()
+    r = torch.randn(N, C, H, W, dtype=torch.float64, requires_grad=True)
+    bn = torch.nn.BatchNorm2d(C).double().train()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C) + 0.5)
+        bn.bias.copy_(torch.randn(C))
+        bn.running_mean.copy_(torch.randn(C))
+        bn.running_var.copy_(torch.rand(C) + 0.5)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    y = bn(x) + (r if res else 0)
+    if relu:
+        y = torch.relu(y)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    nhwc = lambda t: t.detach().permute(0, 2, 3, 1).reshape(P, C).contiguous().float().cuda()  # noqa: E731
+    xd, rd, dyd = nhwc(x), nhwc(r), nhwc(dy)
+    g, b = bn.weight.detach().float().cuda(), bn.bias.detach().float().cuda()
+    rm, rv = rm0.float().cuda(), rv0.float().cuda()
+    yd, mean, inv = torch.empty_like(xd), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    work = torch.empty(int(L.eosv_bn_workspace_bytes(C)) // 4 + 4, device="cuda")
+    _call(L.eosv_bn_train_forward, xd.data_ptr(), P, C, g.data_ptr(), b.data_ptr(), 1e-5, 0.1, rm.data_ptr(),
+          rv.data_ptr(), rd.data_ptr() if res else 0, int(relu), yd.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+          work.data_ptr())
+    dx, dg, db, dres = torch.empty_like(xd), torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty_like(xd)
+    _call(L.eosv_bn_train_backward, dyd.data_ptr(), yd.data_ptr(), int(relu), xd.data_ptr(), P, C, g.data_ptr(),
+          mean.data_ptr(), inv.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), dres.data_ptr(),
+          work.data_ptr())
+
+    def rel(a, bref):
+        return float((a.double().cpu() - bref).norm() / bref.norm())
+
+    back = lambda t: t.view(N, H, W, C).permute(0, 3, 1, 2)  # noqa: E731
+    assert rel(back(yd), y.detach()) < 1e-6
+    assert rel(rm, bn.running_mean) < 1e-6 and rel(rv, bn.running_var) < 1e-6
+    assert rel(back(dx), x.grad) < 1e-5
+    assert rel(dg, bn.weight.grad) < 1e-5 and rel(db, bn.bias.grad) < 1e-5
+    if res:
+        assert rel(back(dres), r.grad) < 1e-6
+
+
+def test_maxpool_forward_backward_vs_torch():
+    from eosv._lib import lib
+
+    L = lib()
+    torch.manual_seed(3)
+    N, C, H, W = 2, 5, 9, 8
+    x = torch.randn(N, C, H, W, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.max_pool2d(x, 3, 2, 1)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    Ho, Wo = y.shape[2], y.shape[3]
+    xd = x.detach().permute(0, 2, 3, 1).contiguous().float().cuda()
+    yd = torch.empty(N * Ho * Wo * C, device="cuda")
+    idx = torch.empty(N * Ho * Wo * C, dtype=torch.int32, device="cuda")
+    _call(L.eosv_maxpool_forward, xd.data_ptr(), N, H, W, C, yd.data_ptr(), idx.data_ptr())
+    dyd = dy.permute(0, 2, 3, 1).contiguous().float().cuda()
+    dx = torch.empty(N * H * W * C, device="cuda")
+    _call(L.eosv_maxpool_backward, dyd.data_ptr(), idx.data_ptr(), N, H, W, C, dx.data_ptr())
+    assert torch.equal(yd.view(N, Ho, Wo, C).permute(0, 3, 1, 2).cpu(), y.detach().float())
+    assert torch.allclose(dx.view(N, H, W, C).permute(0, 3, 1, 2).double().cpu(), x.grad, rtol=0, atol=1e-6)
