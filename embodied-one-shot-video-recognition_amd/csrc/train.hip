@@ -19,7 +19,7 @@
 namespace eosv {
 namespace {
 
-constexpr int BN_CHUNKS = 256;  // row chunks of the two-stage per-channel reductions
+constexpr int BN_CHUNKS = 1024;  // row chunks of the two-stage per-channel reductions
 
 int grid_for(long long n, int block = 256) {
   const long long g = (n + block - 1) / block;
@@ -76,26 +76,32 @@ __global__ void col2im_kernel(const float* __restrict__ col, int N, int H, int W
 }
 
 // per (row chunk, channel): partial sums in double.  MODE 0: x, x^2.  MODE 1 (backward): g, g*xhat
-// with g = dy masked by y > 0 when relu (and written to dres when given)
+// with g = dy masked by y > 0 when relu (and written to dres when given).  A block is TC channel
+// lanes x (256 / TC) row lanes (TC = min(C, 256) rounded to a power of two), reduced in LDS, so
+// narrow layers (C = 64) keep every lane busy.
 template <int MODE>
-__global__ void bn_partials_kernel(const float* __restrict__ a, const float* __restrict__ dy, const float* __restrict__ y,
-                                   int relu, long long P, int C, const float* __restrict__ mean,
-                                   const float* __restrict__ invstd, float* __restrict__ dres,
-                                   double* __restrict__ part) {
+__global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restrict__ a, const float* __restrict__ dy,
+                                                          const float* __restrict__ y, int relu, long long P, int C,
+                                                          int tc, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, float* __restrict__ dres,
+                                                          double* __restrict__ part) {
+  __shared__ double red[2][256];
   const int chunk = blockIdx.y;
   const long long rows = (P + BN_CHUNKS - 1) / BN_CHUNKS;
   const long long r0 = chunk * rows, r1 = min(P, r0 + rows);
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    double s0 = 0.0, s1 = 0.0;
+  const int lc = threadIdx.x % tc, lr = threadIdx.x / tc, nr = blockDim.x / tc;
+  const int c = blockIdx.x * tc + lc;
+  double s0 = 0.0, s1 = 0.0;
+  if (c < C) {
     if (MODE == 0) {
-      for (long long r = r0; r < r1; ++r) {
+      for (long long r = r0 + lr; r < r1; r += nr) {
         const double v = a[r * C + c];
         s0 += v;
         s1 += v * v;
       }
     } else {
       const float m = mean[c], is = invstd[c];
-      for (long long r = r0; r < r1; ++r) {
+      for (long long r = r0 + lr; r < r1; r += nr) {
         float g = dy[r * C + c];
         if (relu && !(y[r * C + c] > 0.f)) g = 0.f;
         if (dres) dres[r * C + c] = g;
@@ -103,9 +109,24 @@ __global__ void bn_partials_kernel(const float* __restrict__ a, const float* __r
         s1 += (double)g * (double)((a[r * C + c] - m) * is);
       }
     }
+  }
+  red[0][threadIdx.x] = s0;
+  red[1][threadIdx.x] = s1;
+  __syncthreads();
+  if (lr == 0 && c < C) {
+    for (int k = 1; k < nr; ++k) {
+      s0 += red[0][k * tc + lc];
+      s1 += red[1][k * tc + lc];
+    }
     part[(long long)chunk * 2 * C + c] = s0;
     part[(long long)chunk * 2 * C + C + c] = s1;
   }
+}
+
+int bn_lanes(int C) {
+  int t = 1;
+  while (t < C && t < 256) t <<= 1;
+  return t;
 }
 
 __global__ void bn_stats_kernel(const double* __restrict__ part, long long P, int C, float eps, float momentum,
@@ -410,8 +431,9 @@ int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gam
     return set_error("eosv_bn_train_forward: bad argument"), EOSV_ERR_ARG;
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
-  hipLaunchKernelGGL((bn_partials_kernel<0>), dim3((C + 255) / 256, BN_CHUNKS), dim3(256), 0, s, d_x, nullptr,
-                     nullptr, 0, (long long)P, C, nullptr, nullptr, nullptr, part);
+  const int tc = bn_lanes(C);
+  hipLaunchKernelGGL((bn_partials_kernel<0>), dim3((C + tc - 1) / tc, BN_CHUNKS), dim3(256), 0, s, d_x, nullptr,
+                     nullptr, 0, (long long)P, C, tc, nullptr, nullptr, nullptr, part);
   hipLaunchKernelGGL(bn_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, (long long)P, C, eps, momentum,
                      d_running_mean, d_running_var, d_save_mean, d_save_invstd);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_x, (long long)P, C,
@@ -429,8 +451,9 @@ int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const 
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
   double* sums = part + (long long)2 * BN_CHUNKS * C;
-  hipLaunchKernelGGL((bn_partials_kernel<1>), dim3((C + 255) / 256, BN_CHUNKS), dim3(256), 0, s, d_x, d_dy, d_y, relu,
-                     (long long)P, C, d_save_mean, d_save_invstd, d_dres, part);
+  const int tc = bn_lanes(C);
+  hipLaunchKernelGGL((bn_partials_kernel<1>), dim3((C + tc - 1) / tc, BN_CHUNKS), dim3(256), 0, s, d_x, d_dy, d_y, relu,
+                     (long long)P, C, tc, d_save_mean, d_save_invstd, d_dres, part);
   hipLaunchKernelGGL(bn_grad_sums_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, C, d_dgamma, d_dbeta, sums);
   hipLaunchKernelGGL(bn_dx_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_dy, d_y, relu, d_x,
                      (long long)P, C, d_gamma, d_save_mean, d_save_invstd, sums, d_dx);

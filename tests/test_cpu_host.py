@@ -292,3 +292,27 @@ def test_dropin_classifier_host_kinds_follow_reference():
         classifier.Classifier("KNN").predict(d)
     with pytest.raises(UnboundLocalError):
         classifier.Classifier("LR").predict(d)
+
+
+def test_train_network_steplr_matches_torch_schedule():
+    """TrainNetwork.lr_at restates StepLR(step_size, 0.1) stepped at the start of each epoch
+    (reference network_train.py:77-84) -- checked against torch's own scheduler, no GPU."""
+    import types
+
+    import network_train
+
+    for step_size in (1, 3, 10):
+        tn = types.SimpleNamespace(lr_1=1e-4, lr_2=1e-3, lr_step_size=step_size)
+        p = torch.nn.Parameter(torch.zeros(1))
+        o1 = torch.optim.SGD([p], lr=1e-4, momentum=0.9)
+        o2 = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=1e-3, momentum=0.9)
+        s1 = torch.optim.lr_scheduler.StepLR(o1, step_size=step_size, gamma=0.1)
+        s2 = torch.optim.lr_scheduler.StepLR(o2, step_size=step_size, gamma=0.1)
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            for epoch in range(12):
+                s1.step()
+                s2.step()
+                l1, l2 = network_train.TrainNetwork.lr_at(tn, epoch)
+                assert abs(l1 - o1.param_groups[0]["lr"]) <= 1e-12 and abs(l2 - o2.param_groups[0]["lr"]) <= 1e-12

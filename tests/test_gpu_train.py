@@ -225,3 +225,68 @@ def test_maxpool_forward_backward_vs_torch():
     _call(L.eosv_maxpool_backward, dyd.data_ptr(), idx.data_ptr(), N, H, W, C, dx.data_ptr())
     assert torch.equal(yd.view(N, Ho, Wo, C).permute(0, 3, 1, 2).cpu(), y.detach().float())
     assert torch.allclose(dx.view(N, H, W, C).permute(0, 3, 1, 2).double().cpu(), x.grad, rtol=0, atol=1e-6)
+
+
+def test_dropin_train_network_checkpoints_follow_reference(tmp_path, monkeypatch):
+    """The drop-in TrainNetwork.finetune_model (network_train.py:52-131) over a 4-video train list,
+    2 epochs of 2 batches, StepLR(step_size=1): every batch the native step sees is recorded and
+    replayed through the torch reference (f64 and f32, SGD momentum, the same lr schedule); the
+    epoch-2 checkpoint must match it under the bounds of test_train_step_matches_torch_reference."""
+    import network_train
+    import utils
+    from eosv import train as etrain
+
+    lines = [l for l in open(utils.TRAIN_LIST).read().splitlines() if l][:2] + \
+            [l for l in open(utils.TRAIN_LIST).read().splitlines() if l][-2:]
+    lst = tmp_path / "train.list"
+    lst.write_text("\n".join(lines) + "\n")
+    monkeypatch.setattr(utils, "IMG_crop_size", (64, 64))
+    monkeypatch.setattr(network_train, "TRAIN_LIST", str(lst))
+    rec = []
+    step0 = etrain.NativeTrainer.step
+
+    def step(self, frames, labels, T, lr_conv, lr_fc, momentum=0.9):
+        rec.append((frames.detach().cpu().clone(), list(np.asarray(labels).reshape(-1)), T, lr_conv, lr_fc))
+        return step0(self, frames, labels, T, lr_conv, lr_fc, momentum)
+
+    monkeypatch.setattr(etrain.NativeTrainer, "step", step)
+    torch.manual_seed(5)
+    tn = network_train.TrainNetwork(str(tmp_path / "loss.txt"), str(tmp_path) + "/ckp/", 2, 2, 1e-3, 1e-2,
+                                    lr_step_size=1, resnet_model="resnet18")
+    init = {k: v.detach().cpu().clone() for k, v in tn.mymodel.state_dict().items()}
+    tn.finetune_model()
+    assert len(rec) == 4 and np.allclose([r[3] for r in rec], [1e-4, 1e-4, 1e-5, 1e-5], rtol=1e-12, atol=0)
+    got = torch.load(str(tmp_path / "ckp" / "model2.pkl"), weights_only=True)
+    assert (tmp_path / "ckp" / "model1.pkl").exists()
+
+    from oracle.resnet_ref import ModelResNetRef
+
+    def replay(dtype):
+        m = ModelResNetRef("resnet18", 64)
+        m.load_state_dict(init)
+        m = m.to(dtype).train()
+        o1 = torch.optim.SGD(m.convnet.parameters(), lr=1e-3, momentum=0.9)
+        o2 = torch.optim.SGD(m.fc.parameters(), lr=1e-2, momentum=0.9)
+        for frames, labels, T, l1, l2 in rec:
+            for g in o1.param_groups:
+                g["lr"] = l1
+            for g in o2.param_groups:
+                g["lr"] = l2
+            o1.zero_grad()
+            o2.zero_grad()
+            f, _ = m(frames.to(dtype))
+            out = m.fc(f.view(len(labels), T, -1).mean(dim=1))
+            torch.nn.CrossEntropyLoss()(out, torch.as_tensor(labels, dtype=torch.long)).backward()
+            o1.step()
+            o2.step()
+        return m.state_dict()
+
+    ref, f32 = replay(torch.float64), replay(torch.float32)
+    for k, v in ref.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(v), k
+            continue
+        v = v.double()
+        err = float((got[k].double() - v).norm())
+        yard = float((f32[k].double() - v).norm())
+        assert err <= max(4 * yard, 1e-6 * v.numel() ** 0.5 + 1e-5 * float(v.norm())), (k, err, yard)
