@@ -320,6 +320,15 @@ __global__ void sum_rows_kernel(const float* __restrict__ x, int rows, int C, fl
   y[c] = accumulate ? y[c] + s : s;
 }
 
+// C[i] = sum over the slices of W (fixed slice order: deterministic)
+__global__ void sum_slices_kernel(const float* __restrict__ w, int slices, long long mn, float* __restrict__ c) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < mn; i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < slices; ++j) s += w[j * mn + i];
+    c[i] = s;
+  }
+}
+
 __global__ void add_bias_kernel(float* __restrict__ y, int rows, int C, const float* __restrict__ b) {
   const long long total = (long long)rows * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -341,6 +350,36 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
 __global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, long long n, float alpha) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] += alpha * x[i];
+}
+
+// W[cout][kh][kw][cin] -> Wf[cin][KH-1-kh][KW-1-kw][cout]: the stride-1 input gradient is the
+// convolution of dY with these weights (same padding for odd square kernels)
+__global__ void flip_weights_kernel(const float* __restrict__ w, int Cout, int KH, int KW, int Cin,
+                                    float* __restrict__ wf) {
+  const long long total = (long long)Cout * KH * KW * Cin;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Cin);
+    const long long r = i / Cin;
+    const int kw = (int)(r % KW);
+    const long long r2 = r / KW;
+    const int kh = (int)(r2 % KH), co = (int)(r2 / KH);
+    wf[(((long long)ci * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Cout + co] = w[i];
+  }
+}
+
+// 64 zero bytes per device: the DMA target of the conv kernels' out-of-bounds taps
+const void* zero_page(int dev) {
+  static std::mutex mu;
+  static void* pages[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!pages[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, 256) != hipSuccess || hipMemset(p, 0, 256) != hipSuccess) return nullptr;
+    pages[dev] = p;
+  }
+  return pages[dev];
 }
 
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int HW, float* __restrict__ y) {
@@ -393,6 +432,53 @@ int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const
                     lda, &beta, d_c, ldc);
   if (st != rocblas_status_success)
     return set_error(std::string("eosv_sgemm: ") + rocblas_status_to_string(st)), EOSV_ERR_HIP;
+  return EOSV_OK;
+}
+
+// split-K plan of C = A^T B: enough slices that the rocBLAS tiles x slices fill the chip,
+// each slice at least 256 reduction rows
+static int splitk_slices(int m, int n, int k) {
+  const long long tiles = (long long)((m + 63) / 64) * ((n + 255) / 256);
+  long long s = (1024 + tiles - 1) / tiles;
+  s = std::min<long long>(s, std::max(1, k / 256));
+  return (int)std::max<long long>(1, std::min<long long>(s, 256));
+}
+
+int64_t eosv_sgemm_tn_splitk_workspace(int m, int n, int k) {
+  if (m <= 0 || n <= 0 || k <= 0) return 0;
+  const int s = splitk_slices(m, n, k);
+  return s > 1 ? (int64_t)s * m * n * (int64_t)sizeof(float) : 0;
+}
+
+int eosv_sgemm_tn_splitk(int m, int n, int k, const float* d_a, int lda, const float* d_b, int ldb, float* d_c,
+                         int ldc, float* d_work, int64_t work_bytes, eosv_stream_t stream) {
+  if (m <= 0 || n <= 0 || k <= 0 || !d_a || !d_b || !d_c || lda < m || ldb < n || ldc != n)
+    return set_error("eosv_sgemm_tn_splitk: bad argument"), EOSV_ERR_ARG;
+  const int want = splitk_slices(m, n, k);
+  if (want == 1 || work_bytes < eosv_sgemm_tn_splitk_workspace(m, n, k) || !d_work)
+    return eosv_sgemm(1, 0, m, n, k, 1.f, d_a, lda, d_b, ldb, 0.f, d_c, ldc, stream);
+  int dev = 0;
+  EOSV_HIP_CHECK(hipGetDevice(&dev));
+  rocblas_handle h = blas_handle(dev);
+  if (!h) return set_error("eosv_sgemm_tn_splitk: rocblas_create_handle failed"), EOSV_ERR_HIP;
+  rocblas_set_stream(h, (hipStream_t)stream);
+  const int kc = (k + want - 1) / want;
+  const int full = k / kc, rem = k - full * kc;
+  const long long mn = (long long)m * n;
+  const float one = 1.f, zero = 0.f;
+  // slice j: W_j^T (n x m, column-major) = B_j (n x kc) . A_j^T, A_j / B_j = rows j*kc.. of A / B
+  rocblas_status st = rocblas_sgemm_strided_batched(
+      h, rocblas_operation_none, rocblas_operation_transpose, n, m, kc, &one, d_b, ldb, (long long)kc * ldb, d_a, lda,
+      (long long)kc * lda, &zero, d_work, n, mn, full);
+  if (st == rocblas_status_success && rem > 0)
+    st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n, m, rem, &one,
+                       d_b + (long long)full * kc * ldb, ldb, d_a + (long long)full * kc * lda, lda, &zero,
+                       d_work + full * mn, n);
+  if (st != rocblas_status_success)
+    return set_error(std::string("eosv_sgemm_tn_splitk: ") + rocblas_status_to_string(st)), EOSV_ERR_HIP;
+  hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(mn)), dim3(256), 0, (hipStream_t)stream, d_work,
+                     full + (rem > 0), mn, d_c);
+  EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
 
@@ -537,6 +623,45 @@ int eosv_sgd_momentum(float* d_p, const float* d_g, float* d_buf, int64_t n, flo
 int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_t stream) {
   if (!d_y || !d_x || n <= 0) return set_error("eosv_axpy: bad argument"), EOSV_ERR_ARG;
   hipLaunchKernelGGL(axpy_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d_y, d_x, (long long)n, alpha);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_w, int Cout, int KH, int KW,
+                    int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y,
+                    eosv_stream_t stream) {
+  if (!d_x || !d_w || !d_y || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || KH <= 0 || KW <= 0 ||
+      stride <= 0 || pad < 0)
+    return set_error("eosv_conv2d_f32: bad argument"), EOSV_ERR_ARG;
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return set_error("eosv_conv2d_f32: empty output"), EOSV_ERR_ARG;
+  if (Cin == 3 || Cin % 32 || (KH * KW * Cin) % 32)
+    return set_error("eosv_conv2d_f32: needs Cin % 32 == 0 (the stem goes through im2col + eosv_sgemm)"),
+           EOSV_ERR_UNSUPPORTED;
+  int dev = 0;
+  EOSV_HIP_CHECK(hipGetDevice(&dev));
+  ConvArgs a{};
+  a.x = d_x;
+  a.w = d_w;
+  a.bias = d_bias;
+  a.res = d_res;
+  a.y = d_y;
+  a.N = N, a.H = H, a.W = W, a.Cin = Cin;
+  a.Ho = Ho, a.Wo = Wo, a.Cout = Cout;
+  a.KH = KH, a.KW = KW, a.KWp = KW, a.stride = stride, a.pad = pad;
+  a.K = KH * KW * Cin;
+  a.relu = relu;
+  a.zero = zero_page(dev);
+  a.xcd = 1;
+  if (!a.zero) return set_error("eosv_conv2d_f32: zero page allocation failed"), EOSV_ERR_OOM;
+  return launch_conv_f32(a, (hipStream_t)stream);
+}
+
+int eosv_flip_weights(const float* d_w, int Cout, int KH, int KW, int Cin, float* d_wf, eosv_stream_t stream) {
+  if (!d_w || !d_wf || Cout <= 0 || KH <= 0 || KW <= 0 || Cin <= 0)
+    return set_error("eosv_flip_weights: bad argument"), EOSV_ERR_ARG;
+  hipLaunchKernelGGL(flip_weights_kernel, dim3(grid_for((long long)Cout * KH * KW * Cin)), dim3(256), 0,
+                     (hipStream_t)stream, d_w, Cout, KH, KW, Cin, d_wf);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

@@ -30,7 +30,8 @@ EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_ba
            "eosv_sgemm", "eosv_im2col", "eosv_col2im", "eosv_bn_workspace_bytes", "eosv_bn_train_forward",
            "eosv_bn_train_backward", "eosv_maxpool_forward", "eosv_maxpool_backward", "eosv_avgpool_forward",
            "eosv_broadcast_rows", "eosv_softmax_xent", "eosv_sum_rows", "eosv_add_bias", "eosv_sgd_momentum",
-           "eosv_axpy", "eosv_nchw_to_nhwc")
+           "eosv_axpy", "eosv_nchw_to_nhwc", "eosv_conv2d_f32", "eosv_flip_weights",
+           "eosv_sgemm_tn_splitk_workspace", "eosv_sgemm_tn_splitk")
 
 
 class EosvDesc(ctypes.Structure):
@@ -94,6 +95,10 @@ def lib():
         "eosv_sgd_momentum": (i32, [vp, vp, vp, i64, f32, f32, i32, vp]),
         "eosv_axpy": (i32, [vp, vp, i64, f32, vp]),
         "eosv_nchw_to_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+        "eosv_conv2d_f32": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp]),
+        "eosv_flip_weights": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+        "eosv_sgemm_tn_splitk_workspace": (i64, [i32, i32, i32]),
+        "eosv_sgemm_tn_splitk": (i32, [i32, i32, i32, vp, i32, vp, i32, vp, i32, vp, i64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

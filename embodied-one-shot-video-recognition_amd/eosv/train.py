@@ -24,6 +24,7 @@ from . import arch as _arch
 from ._lib import check, lib, ptr, stream_ptr
 
 BN_EPS = 1e-5
+_UNSUPPORTED = -4  # EOSV_ERR_UNSUPPORTED
 BN_MOMENTUM = 0.1
 
 
@@ -177,14 +178,20 @@ class NativeTrainer:
         N, H, W, _ = shape
         Ho, Wo = (H + 2 * c.pad - c.k) // c.stride + 1, (W + 2 * c.pad - c.k) // c.stride + 1
         P = N * Ho * Wo
-        if c.k == 1 and c.stride == 1:
-            col = x
-        else:
-            col = self._buf("col", P * c.K)
-            check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
         y = torch.empty(P * c.cout, dtype=torch.float32, device=self.dev)
-        check(self.L.eosv_sgemm(0, 1, P, c.cout, c.K, 1.0, _f(col), c.K, _f(c.w), c.K, 0.0, _f(y), c.cout, s),
-              "eosv_sgemm")
+        # the inference conv kernels (exact-f32 MFMA) where they apply, else im2col + rocBLAS
+        rc = self.L.eosv_conv2d_f32(_f(x), N, H, W, c.cin, _f(c.w), c.cout, c.k, c.k, c.stride, c.pad, None, None, 0,
+                                    _f(y), s)
+        if rc == _UNSUPPORTED:
+            if c.k == 1 and c.stride == 1:
+                col = x
+            else:
+                col = self._buf("col", P * c.K)
+                check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
+            check(self.L.eosv_sgemm(0, 1, P, c.cout, c.K, 1.0, _f(col), c.K, _f(c.w), c.K, 0.0, _f(y), c.cout, s),
+                  "eosv_sgemm")
+        else:
+            check(rc, "eosv_conv2d_f32")
         return y, (N, Ho, Wo, c.cout)
 
     def _conv_bwd(self, dz, x, shape, c: _Conv, s, need_dx=True):
@@ -198,11 +205,22 @@ class NativeTrainer:
         else:
             col = self._buf("col", P * c.K)
             check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
-        check(self.L.eosv_sgemm(1, 0, c.cout, c.K, P, 1.0, _f(dz), c.cout, _f(col), c.K, 0.0, _f(c.g), c.K, s),
-              "eosv_sgemm")
+        wb = int(self.L.eosv_sgemm_tn_splitk_workspace(c.cout, c.K, P))
+        ws = self._buf("splitk", wb // 4 + 1)
+        check(self.L.eosv_sgemm_tn_splitk(c.cout, c.K, P, _f(dz), c.cout, _f(col), c.K, _f(c.g), c.K, _f(ws), wb, s),
+              "eosv_sgemm_tn_splitk")
         if not need_dx:
             return None
         dx = torch.empty(N * H * W * c.cin, dtype=torch.float32, device=self.dev)
+        if c.stride == 1 and c.k % 2 == 1 and c.pad == c.k // 2:
+            # stride 1: dx = conv(dz, W flipped and transposed) on the inference conv kernels
+            wf = self._buf("wflip", c.cout * c.K)
+            check(self.L.eosv_flip_weights(_f(c.w), c.cout, c.k, c.k, c.cin, _f(wf), s), "eosv_flip_weights")
+            rc = self.L.eosv_conv2d_f32(_f(dz), N, Ho, Wo, c.cout, _f(wf), c.cin, c.k, c.k, 1, c.pad, None, None, 0,
+                                        _f(dx), s)
+            if rc != _UNSUPPORTED:
+                check(rc, "eosv_conv2d_f32")
+                return dx
         dcol = dx if direct else self._buf("dcol", P * c.K)
         check(self.L.eosv_sgemm(0, 0, P, c.K, c.cout, 1.0, _f(dz), c.cout, _f(c.w), c.K, 0.0, _f(dcol), c.K, s),
               "eosv_sgemm")

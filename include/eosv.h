@@ -190,6 +190,13 @@ int eosv_backbone_probe(eosv_handle* h, const float* d_frames, int B, int stage,
  * dW = dY^T Xcol (loss.backward(), network_train.py:114). */
 int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* d_a, int lda,
                const float* d_b, int ldb, float beta, float* d_c, int ldc, eosv_stream_t stream);
+/* Weight-gradient GEMM C[m][n] = A^T B with A [k][m], B [k][n] row-major and k (the pixel count
+ * P of a conv) much larger than m, n: the reduction is split into slices, each a strided-batched
+ * rocBLAS GEMM into d_work, then summed in a fixed order (deterministic).  work_bytes below
+ * eosv_sgemm_tn_splitk_workspace(m, n, k) falls back to one eosv_sgemm.  ldc must equal n. */
+int64_t eosv_sgemm_tn_splitk_workspace(int m, int n, int k);
+int eosv_sgemm_tn_splitk(int m, int n, int k, const float* d_a, int lda, const float* d_b, int ldb, float* d_c,
+                         int ldc, float* d_work, int64_t work_bytes, eosv_stream_t stream);
 /* im2col of NHWC x: col[(n, oh, ow)][(kh, kw, c)], zero padding; col2im is its adjoint
  * (gather-sum, overwrites d_x). */
 int eosv_im2col(const float* d_x, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_col,
@@ -228,6 +235,14 @@ int eosv_add_bias(float* d_y, int rows, int C, const float* d_bias, eosv_stream_
 /* torch.optim.SGD step (momentum, dampening 0): buf = first ? g : momentum buf + g; p -= lr buf. */
 int eosv_sgd_momentum(float* d_p, const float* d_g, float* d_buf, int64_t n, float lr, float momentum, int first,
                       eosv_stream_t stream);
+/* Direct f32 convolution of NHWC d_x with d_w [Cout][KH][KW][Cin] (+ bias, + residual, ReLU) on
+ * the inference conv kernels (exact-f32 MFMA implicit GEMM / stage-1 row kernel): the train-mode
+ * forward of every conv but the stem, and, with eosv_flip_weights' [Cin][KH][KW][Cout] weights,
+ * the input gradient of the stride-1 convs.  EOSV_ERR_UNSUPPORTED unless Cin % 32 == 0. */
+int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_w, int Cout, int KH, int KW,
+                    int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y,
+                    eosv_stream_t stream);
+int eosv_flip_weights(const float* d_w, int Cout, int KH, int KW, int Cin, float* d_wf, eosv_stream_t stream);
 /* y += alpha x; NCHW -> NHWC. */
 int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_t stream);
 int eosv_nchw_to_nhwc(const float* d_x, int N, int C, int H, int W, float* d_y, eosv_stream_t stream);

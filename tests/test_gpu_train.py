@@ -154,6 +154,52 @@ def test_conv_forward_and_gradients_vs_torch(k, stride, pad, cin, cout):
     assert rel(gx.view(N, H, W, cin).permute(0, 3, 1, 2), x.grad) < 1e-5
 
 
+@pytest.mark.parametrize("k,stride,cin,cout,H", [(3, 1, 64, 64, 56), (3, 1, 128, 64, 14), (1, 1, 64, 256, 28),
+                                                 (3, 2, 64, 128, 28), (1, 2, 256, 512, 14)])
+def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
+    """The trainer's fast paths: eosv_conv2d_f32 forward (the inference conv kernels, exact f32),
+    the stride-1 input gradient as a conv of dY with eosv_flip_weights' weights, and the
+    split-K weight gradient eosv_sgemm_tn_splitk (ragged last slice), against f64 autograd."""
+    from eosv._lib import lib
+
+    L = lib()
+    torch.manual_seed(2)
+    N, pad = 3, k // 2
+    x = torch.randn(N, cin, H, H, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, k, k, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, stride=stride, padding=pad)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    Ho, Wo = y.shape[2], y.shape[3]
+    P, K = N * Ho * Wo, k * k * cin
+    xd = x.detach().permute(0, 2, 3, 1).contiguous().float().cuda()
+    wd = w.detach().permute(0, 2, 3, 1).reshape(cout, K).contiguous().float().cuda()
+    dyd = dy.permute(0, 2, 3, 1).reshape(P, cout).contiguous().float().cuda()
+
+    def rel(a, b):
+        return float((a.double().cpu() - b).norm() / b.norm())
+
+    yd = torch.empty(P * cout, device="cuda")
+    _call(L.eosv_conv2d_f32, xd.data_ptr(), N, H, H, cin, wd.data_ptr(), cout, k, k, stride, pad, None, None, 0,
+          yd.data_ptr())
+    assert rel(yd.view(N, Ho, Wo, cout).permute(0, 3, 1, 2), y.detach()) < 1e-5
+    col = torch.empty(P * K, device="cuda")
+    _call(L.eosv_im2col, xd.data_ptr(), N, H, H, cin, k, k, stride, pad, col.data_ptr())
+    wb = int(L.eosv_sgemm_tn_splitk_workspace(cout, K, P))
+    ws = torch.empty(wb // 4 + 1, device="cuda")
+    gw = torch.empty(cout * K, device="cuda")
+    _call(L.eosv_sgemm_tn_splitk, cout, K, P, dyd.data_ptr(), cout, col.data_ptr(), K, gw.data_ptr(), K,
+          ws.data_ptr(), wb)
+    assert rel(gw.view(cout, k, k, cin).permute(0, 3, 1, 2), w.grad) < 1e-5
+    if stride == 1:
+        wf = torch.empty(cout * K, device="cuda")
+        _call(L.eosv_flip_weights, wd.data_ptr(), cout, k, k, cin, wf.data_ptr())
+        gx = torch.empty(N * H * H * cin, device="cuda")
+        _call(L.eosv_conv2d_f32, dyd.data_ptr(), N, Ho, Wo, cout, wf.data_ptr(), cin, k, k, 1, pad, None, None, 0,
+              gx.data_ptr())
+        assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad) < 1e-5
+
+
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
 def test_batchnorm_train_forward_backward_vs_torch(relu, res):
     """eosv_bn_train_forward / _backward against nn.BatchNorm2d in train mode (f64 autograd):
