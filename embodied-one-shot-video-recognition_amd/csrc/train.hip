@@ -84,10 +84,10 @@ __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restric
                                                           const float* __restrict__ y, int relu, long long P, int C,
                                                           int tc, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, float* __restrict__ dres,
-                                                          double* __restrict__ part) {
+                                                          int chunks, double* __restrict__ part) {
   __shared__ double red[2][256];
   const int chunk = blockIdx.y;
-  const long long rows = (P + BN_CHUNKS - 1) / BN_CHUNKS;
+  const long long rows = (P + chunks - 1) / chunks;
   const long long r0 = chunk * rows, r1 = min(P, r0 + rows);
   const int lc = threadIdx.x % tc, lr = threadIdx.x / tc, nr = blockDim.x / tc;
   const int c = blockIdx.x * tc + lc;
@@ -129,24 +129,124 @@ int bn_lanes(int C) {
   return t;
 }
 
-__global__ void bn_stats_kernel(const double* __restrict__ part, long long P, int C, float eps, float momentum,
-                                float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean,
-                                float* __restrict__ invstd) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// row chunks of the two-stage reductions: enough blocks to fill the chip, at least 4 rows per lane
+int bn_chunks(long long P, int C) {
+  const int tc = bn_lanes(C), nr = 256 / tc, cblocks = (C + tc - 1) / tc;
+  long long k = (2048 + cblocks - 1) / cblocks;
+  k = std::min<long long>(k, std::max<long long>(1, P / (4LL * nr)));
+  return (int)std::max<long long>(1, std::min<long long>(k, BN_CHUNKS));
+}
+
+// the second stage: 16 channel lanes x 16 chunk lanes per block (fixed order, deterministic), then
+// MODE 0 the batch statistics and running estimates, MODE 1 dgamma / dbeta and the sums for dx
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int chunks, long long P,
+                                                          int C, float eps, float momentum, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar, float* __restrict__ out0,
+                                                          float* __restrict__ out1, double* __restrict__ sums) {
+  __shared__ double red[2][16][17];
+  const int lc = threadIdx.x & 15, lk = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + lc;
   double s0 = 0.0, s1 = 0.0;
-  for (int k = 0; k < BN_CHUNKS; ++k) {
-    s0 += part[(long long)k * 2 * C + c];
-    s1 += part[(long long)k * 2 * C + C + c];
+  if (c < C)
+    for (int k = lk; k < chunks; k += 16) {
+      s0 += part[(long long)k * 2 * C + c];
+      s1 += part[(long long)k * 2 * C + C + c];
+    }
+  red[0][lk][lc] = s0;
+  red[1][lk][lc] = s1;
+  __syncthreads();
+  if (lk != 0 || c >= C) return;
+  for (int j = 1; j < 16; ++j) {
+    s0 += red[0][j][lc];
+    s1 += red[1][j][lc];
   }
-  const double m = s0 / (double)P;
-  const double var = fmax(s1 / (double)P - m * m, 0.0);  // biased: used to normalise
-  mean[c] = (float)m;
-  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (rmean) {
-    const double unb = P > 1 ? var * (double)P / (double)(P - 1) : var;  // unbiased: running estimate
-    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
-    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  if (MODE == 0) {
+    const double m = s0 / (double)P;
+    const double var = fmax(s1 / (double)P - m * m, 0.0);  // biased: used to normalise
+    out0[c] = (float)m;
+    out1[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) {
+      const double unb = P > 1 ? var * (double)P / (double)(P - 1) : var;  // unbiased: running estimate
+      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  } else {
+    out0[c] = (float)s1;  // dgamma
+    out1[c] = (float)s0;  // dbeta
+    sums[c] = s0;
+    sums[C + c] = s1;
+  }
+}
+
+// elementwise passes: C/4 float4 channel lanes x row lanes per block, per-channel operands held
+// in registers across the rows (C % 4 == 0 and 16-byte aligned operands; else the scalar kernels)
+__device__ inline float4 ld4(const float* p, int c4) { return reinterpret_cast<const float4*>(p)[c4]; }
+
+__global__ __launch_bounds__(256) void bn_apply4_kernel(const float4* __restrict__ x, long long P, int C4,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        const float4* __restrict__ res, int relu,
+                                                        float4* __restrict__ y) {
+  const int lanes = min(C4, 256), nr = 256 / lanes;
+  const int lc = threadIdx.x % lanes, lr = threadIdx.x / lanes;
+  if (lr >= nr) return;
+  for (int c4 = lc; c4 < C4; c4 += lanes) {
+    const float4 m = ld4(mean, c4), is = ld4(invstd, c4), g = ld4(gamma, c4), b = ld4(beta, c4);
+    for (long long r = (long long)blockIdx.x * nr + lr; r < P; r += (long long)gridDim.x * nr) {
+      const long long i = r * C4 + c4;
+      const float4 v = x[i];
+      float4 o;
+      o.x = (v.x - m.x) * is.x * g.x + b.x;
+      o.y = (v.y - m.y) * is.y * g.y + b.y;
+      o.z = (v.z - m.z) * is.z * g.z + b.z;
+      o.w = (v.w - m.w) * is.w * g.w + b.w;
+      if (res) {
+        const float4 q = res[i];
+        o.x += q.x, o.y += q.y, o.z += q.z, o.w += q.w;
+      }
+      if (relu) o.x = fmaxf(o.x, 0.f), o.y = fmaxf(o.y, 0.f), o.z = fmaxf(o.z, 0.f), o.w = fmaxf(o.w, 0.f);
+      y[i] = o;
+    }
+  }
+}
+
+__device__ inline float bn_dx1(float dy, float y, int relu, float x, float m, float is, float g, float mg,
+                               float mgx) {
+  if (relu && !(y > 0.f)) dy = 0.f;
+  const float xhat = (x - m) * is;
+  return g * is * (dy - mg - xhat * mgx);
+}
+
+__global__ __launch_bounds__(256) void bn_dx4_kernel(const float4* __restrict__ dy, const float4* __restrict__ y,
+                                                     int relu, const float4* __restrict__ x, long long P, int C4,
+                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd,
+                                                     const double* __restrict__ sums, float4* __restrict__ dx) {
+  const int lanes = min(C4, 256), nr = 256 / lanes;
+  const int lc = threadIdx.x % lanes, lr = threadIdx.x / lanes;
+  if (lr >= nr) return;
+  const int C = 4 * C4;
+  for (int c4 = lc; c4 < C4; c4 += lanes) {
+    const float4 m = ld4(mean, c4), is = ld4(invstd, c4), g = ld4(gamma, c4);
+    float mg[4], mgx[4];
+    for (int j = 0; j < 4; ++j) {
+      mg[j] = (float)(sums[4 * c4 + j] / (double)P);
+      mgx[j] = (float)(sums[C + 4 * c4 + j] / (double)P);
+    }
+    for (long long r = (long long)blockIdx.x * nr + lr; r < P; r += (long long)gridDim.x * nr) {
+      const long long i = r * C4 + c4;
+      const float4 d = dy[i], v = x[i];
+      const float4 yy = relu ? y[i] : make_float4(1.f, 1.f, 1.f, 1.f);
+      float4 o;
+      o.x = bn_dx1(d.x, yy.x, relu, v.x, m.x, is.x, g.x, mg[0], mgx[0]);
+      o.y = bn_dx1(d.y, yy.y, relu, v.y, m.y, is.y, g.y, mg[1], mgx[1]);
+      o.z = bn_dx1(d.z, yy.z, relu, v.z, m.z, is.z, g.z, mg[2], mgx[2]);
+      o.w = bn_dx1(d.w, yy.w, relu, v.w, m.w, is.w, g.w, mg[3], mgx[3]);
+      dx[i] = o;
+    }
   }
 }
 
@@ -165,21 +265,6 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, long long P, int C,
   }
 }
 
-__global__ void bn_grad_sums_kernel(const double* __restrict__ part, int C, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta, double* __restrict__ sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s0 = 0.0, s1 = 0.0;
-  for (int k = 0; k < BN_CHUNKS; ++k) {
-    s0 += part[(long long)k * 2 * C + c];
-    s1 += part[(long long)k * 2 * C + C + c];
-  }
-  dbeta[c] = (float)s0;
-  dgamma[c] = (float)s1;
-  sums[c] = s0;
-  sums[C + c] = s1;
-}
-
 // dx = gamma * invstd * (g - sum(g) / P - xhat * sum(g * xhat) / P)
 __global__ void bn_dx_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu,
                              const float* __restrict__ x, long long P, int C, const float* __restrict__ gamma,
@@ -189,12 +274,16 @@ __global__ void bn_dx_kernel(const float* __restrict__ dy, const float* __restri
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
-    float g = dy[i];
-    if (relu && !(y[i] > 0.f)) g = 0.f;
-    const float xhat = (x[i] - mean[c]) * invstd[c];
-    const float mg = (float)(sums[c] / (double)P), mgx = (float)(sums[C + c] / (double)P);
-    dx[i] = gamma[c] * invstd[c] * (g - mg - xhat * mgx);
+    dx[i] = bn_dx1(dy[i], relu ? y[i] : 1.f, relu, x[i], mean[c], invstd[c], gamma[c], (float)(sums[c] / (double)P),
+                   (float)(sums[C + c] / (double)P));
   }
+}
+
+bool al16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; }
+
+int rows_grid(long long P, int C) {
+  const int nr = 256 / std::min(C / 4, 256);
+  return (int)std::min<long long>((P + nr - 1) / nr, 4096);
 }
 
 // 3x3 / 2, pad 1 (torchvision's maxpool); argmax = first maximum in (kh, kw) order, as torch CPU
@@ -439,8 +528,9 @@ int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const
 // each slice at least 256 reduction rows
 static int splitk_slices(int m, int n, int k) {
   const long long tiles = (long long)((m + 63) / 64) * ((n + 255) / 256);
-  long long s = (1024 + tiles - 1) / tiles;
-  s = std::min<long long>(s, std::max(1, k / 256));
+  const long long target = env_switch("EOSV_SPLITK_TARGET", 256);
+  long long s = (target + tiles - 1) / tiles;
+  s = std::min<long long>(s, std::max(1, k / env_switch("EOSV_SPLITK_MINROWS", 1024)));
   return (int)std::max<long long>(1, std::min<long long>(s, 256));
 }
 
@@ -517,13 +607,19 @@ int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gam
     return set_error("eosv_bn_train_forward: bad argument"), EOSV_ERR_ARG;
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
-  const int tc = bn_lanes(C);
-  hipLaunchKernelGGL((bn_partials_kernel<0>), dim3((C + tc - 1) / tc, BN_CHUNKS), dim3(256), 0, s, d_x, nullptr,
-                     nullptr, 0, (long long)P, C, tc, nullptr, nullptr, nullptr, part);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, (long long)P, C, eps, momentum,
-                     d_running_mean, d_running_var, d_save_mean, d_save_invstd);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_x, (long long)P, C,
-                     d_save_mean, d_save_invstd, d_gamma, d_beta, d_residual, relu, d_y);
+  const int tc = bn_lanes(C), chunks = bn_chunks(P, C);
+  hipLaunchKernelGGL((bn_partials_kernel<0>), dim3((C + tc - 1) / tc, chunks), dim3(256), 0, s, d_x, nullptr, nullptr,
+                     0, (long long)P, C, tc, nullptr, nullptr, nullptr, chunks, part);
+  hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3((C + 15) / 16), dim3(256), 0, s, part, chunks, (long long)P, C, eps,
+                     momentum, d_running_mean, d_running_var, d_save_mean, d_save_invstd, nullptr);
+  if (C % 4 == 0 && al16(d_x) && al16(d_y) && al16(d_residual) && al16(d_save_mean) && al16(d_save_invstd) &&
+      al16(d_gamma) && al16(d_beta))
+    hipLaunchKernelGGL(bn_apply4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)d_x, (long long)P,
+                       C / 4, d_save_mean, d_save_invstd, d_gamma, d_beta, (const float4*)d_residual, relu,
+                       (float4*)d_y);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_x, (long long)P, C,
+                       d_save_mean, d_save_invstd, d_gamma, d_beta, d_residual, relu, d_y);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -537,12 +633,19 @@ int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const 
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
   double* sums = part + (long long)2 * BN_CHUNKS * C;
-  const int tc = bn_lanes(C);
-  hipLaunchKernelGGL((bn_partials_kernel<1>), dim3((C + tc - 1) / tc, BN_CHUNKS), dim3(256), 0, s, d_x, d_dy, d_y, relu,
-                     (long long)P, C, tc, d_save_mean, d_save_invstd, d_dres, part);
-  hipLaunchKernelGGL(bn_grad_sums_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, C, d_dgamma, d_dbeta, sums);
-  hipLaunchKernelGGL(bn_dx_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_dy, d_y, relu, d_x,
-                     (long long)P, C, d_gamma, d_save_mean, d_save_invstd, sums, d_dx);
+  const int tc = bn_lanes(C), chunks = bn_chunks(P, C);
+  hipLaunchKernelGGL((bn_partials_kernel<1>), dim3((C + tc - 1) / tc, chunks), dim3(256), 0, s, d_x, d_dy, d_y, relu,
+                     (long long)P, C, tc, d_save_mean, d_save_invstd, d_dres, chunks, part);
+  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3((C + 15) / 16), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f,
+                     0.f, nullptr, nullptr, d_dgamma, d_dbeta, sums);
+  if (C % 4 == 0 && al16(d_dy) && al16(d_y) && al16(d_x) && al16(d_dx) && al16(d_gamma) && al16(d_save_mean) &&
+      al16(d_save_invstd))
+    hipLaunchKernelGGL(bn_dx4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)d_dy,
+                       (const float4*)d_y, relu, (const float4*)d_x, (long long)P, C / 4, d_gamma, d_save_mean,
+                       d_save_invstd, sums, (float4*)d_dx);
+  else
+    hipLaunchKernelGGL(bn_dx_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_dy, d_y, relu, d_x,
+                       (long long)P, C, d_gamma, d_save_mean, d_save_invstd, sums, d_dx);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
