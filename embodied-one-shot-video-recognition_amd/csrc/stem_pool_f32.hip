@@ -22,6 +22,11 @@
 // a step whose 4 k straddle two kernel rows picks the row base per lane (one v_cndmask
 // between two wave-uniform bases), so it is one ds_read_b32 per lane and tile.
 //
+// Row bands: a workgroup computes pooled rows [py0, py1) of one image (grid = images x bands),
+// starting with stem row 2 py0 - 1 -- one stem row recomputed per band.  One workgroup per image
+// left the last wave of a launch mostly empty (~2400 frames on 768 slots: 3.1 rounds -> 4);
+// the launcher picks the band count that minimises rounds x rows per band.
+//
 // LDS: a ring of 13 input rows (row r in slot r % 13; a step needs rows 4py .. 4py+8 and
 // prefetches 4py+9 .. 4py+12), each row Wp * 3 floats padded to 16 B, filled by LDS-DMA from
 // the dense padded RGB pack (8-B aligned sources): ~36 KiB at 224, so several workgroups share
@@ -70,14 +75,17 @@ template <bool SPLIT, int NT>
 __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ bias, void* y, int H,
-                                                                 int W, int Hs, int Ws, int Hq, int Wq) {
+                                                                 int W, int Hs, int Ws, int Hq, int Wq, int bands) {
   extern __shared__ __attribute__((aligned(16))) float spf_smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int g = tid >> 6;  // output-channel group
   const int r16 = lane & 15;
   const int q = lane >> 4;
-  const int img = blockIdx.x;
+  const int img = blockIdx.x / bands, band = blockIdx.x - bands * img;
+  const int rpb = (Hq + bands - 1) / bands;  // pooled rows per band
+  const int py0 = band * rpb, py1 = min(Hq, py0 + rpb);
+  if (py0 >= py1) return;
   const int Wp = stem_row_pixels(W, 3);
   const int RF = spf_row_floats(Wp);  // ring row stride (floats)
   const int Hpad = H + 6;
@@ -135,20 +143,37 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
     }
   };
 
-  stage(0, SPF_RING);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
   const float NEG = -INFINITY;
   f32x4 prev[NT];  // stem row 2py - 1
 #pragma unroll
   for (int k = 0; k < NT; ++k) prev[k] = f32x4{NEG, NEG, NEG, NEG};
+  if (py0 == 0) {
+    stage(0, SPF_RING);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    // a band below the top starts with stem row 2 py0 - 1 (input rows 4 py0 - 2 .. 4 py0 + 4);
+    // rows up to 4 py0 + 8 are the first step's
+    stage(4 * py0 - 2, 11);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x4 a0[NT];
+    stem_row(2 * py0 - 1, a0);
+    const bool ok0 = 2 * py0 - 1 < Hs;
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) prev[k][e] = ok0 && colok[k] ? a0[k][e] : NEG;
+    // every wave is done with rows 4 py0 - 2, 4 py0 - 1 before the first step's DMA reuses their slots
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   float* yimg = (float*)y + (long long)img * Hq * Wq * 64;
   unsigned short* ysp = (unsigned short*)y + (long long)img * Hq * Wq * 128;
   const bool even = !(r16 & 1);
 
-  for (int py = 0; py < Hq; ++py) {
-    if (py + 1 < Hq) stage(4 * py + 9, 4);
+  for (int py = py0; py < py1; ++py) {
+    if (py + 1 < py1) stage(4 * py + 9, 4);
     f32x4 a1[NT], a2[NT];
     stem_row(2 * py, a1);
     stem_row(2 * py + 1, a2);
@@ -204,6 +229,22 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// bands per image: fewest (rounds of the grid over the chip's slots) x (stem rows per band)
+static int spf_bands(int B, int Hq, int occ) {
+  static const int forced = env_switch("EOSV_STEM_BANDS", 0);  // profiling build: fixed band count
+  if (forced > 0) return forced;
+  const long long slots = (long long)std::max(occ, 1) * device_cu_count();
+  int best = 1;
+  long long best_cost = -1;
+  for (int b = 1; b <= 8 && b <= Hq; ++b) {
+    const int rpb = (Hq + b - 1) / b;
+    const long long rounds = ((long long)B * b + slots - 1) / slots;
+    const long long cost = rounds * (2LL * rpb + (b > 1));
+    if (best_cost < 0 || cost < best_cost) best = b, best_cost = cost;
+  }
+  return best;
+}
+
 bool stem_pool_f32_ok(int H, int W) {
   const int Ws = (W + 6 - 7) / 2 + 1;
   return H >= 8 && W >= 8 && (Ws + 15) / 16 <= SPF_MAX_TILES;
@@ -211,18 +252,18 @@ bool stem_pool_f32_ok(int H, int W) {
 
 template <bool SPLIT, int NT>
 static void launch_nt(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                      hipStream_t s, size_t lds, int Hs, int Ws, int Hq, int Wq) {
-  hipLaunchKernelGGL((stem_pool_f32_kernel<SPLIT, NT>), dim3(B), dim3(SPF_NT), lds, s, (const float*)pack,
-                     (const float*)w, bias, y, H, W, Hs, Ws, Hq, Wq);
+                      hipStream_t s, size_t lds, int Hs, int Ws, int Hq, int Wq, int bands) {
+  hipLaunchKernelGGL((stem_pool_f32_kernel<SPLIT, NT>), dim3(B * bands), dim3(SPF_NT), lds, s, (const float*)pack,
+                     (const float*)w, bias, y, H, W, Hs, Ws, Hq, Wq, bands);
 }
 
 template <bool SPLIT>
 static void launch_split(int nt, const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                         hipStream_t s, size_t lds, int Hs, int Ws, int Hq, int Wq) {
+                         hipStream_t s, size_t lds, int Hs, int Ws, int Hq, int Wq, int bands) {
   switch (nt) {
 #define EOSV_SPF_NT(n) \
   case n:              \
-    return launch_nt<SPLIT, n>(pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq);
+    return launch_nt<SPLIT, n>(pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
     EOSV_SPF_NT(1) EOSV_SPF_NT(2) EOSV_SPF_NT(3) EOSV_SPF_NT(4) EOSV_SPF_NT(5) EOSV_SPF_NT(6) EOSV_SPF_NT(7)
     EOSV_SPF_NT(8)
 #undef EOSV_SPF_NT
@@ -238,14 +279,13 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
   if (!stem_pool_f32_ok(H, W)) return set_error("stem_pool_f32: unsupported frame size"), EOSV_ERR_UNSUPPORTED;
   const size_t lds = (size_t)(SPF_RING * spf_row_floats(stem_row_pixels(W, 3)) + SPF_SLACK) * 4;
   if (lds > 163840) return set_error("stem_pool_f32: rows too wide for LDS"), EOSV_ERR_UNSUPPORTED;
-  if (info) {
-    static const int occ = kernel_occupancy((const void*)stem_pool_f32_kernel<false, 7>, SPF_NT, lds);
-    return record_launch(info, B, occ);
-  }
+  static const int occ = kernel_occupancy((const void*)stem_pool_f32_kernel<false, 7>, SPF_NT, lds);
+  const int bands = spf_bands(B, Hq, occ);
+  if (info) return record_launch(info, B * bands, occ);
   if (split)
-    launch_split<true>(nt, pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq);
+    launch_split<true>(nt, pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
   else
-    launch_split<false>(nt, pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq);
+    launch_split<false>(nt, pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

@@ -75,51 +75,90 @@ __global__ void col2im_kernel(const float* __restrict__ col, int N, int H, int W
   }
 }
 
+// V consecutive floats (V = 4: one 16-byte access)
+template <int V>
+__device__ inline void ldv(const float* __restrict__ p, long long i, float (&o)[V]) {
+  if constexpr (V == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p + i);
+    o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = v.w;
+  } else {
+    for (int j = 0; j < V; ++j) o[j] = p[i + j];
+  }
+}
+template <int V>
+__device__ inline void stv(float* __restrict__ p, long long i, const float (&o)[V]) {
+  if constexpr (V == 4) {
+    *reinterpret_cast<float4*>(p + i) = make_float4(o[0], o[1], o[2], o[3]);
+  } else {
+    for (int j = 0; j < V; ++j) p[i + j] = o[j];
+  }
+}
+
 // per (row chunk, channel): partial sums in double.  MODE 0: x, x^2.  MODE 1 (backward): g, g*xhat
-// with g = dy masked by y > 0 when relu (and written to dres when given).  A block is TC channel
-// lanes x (256 / TC) row lanes (TC = min(C, 256) rounded to a power of two), reduced in LDS, so
-// narrow layers (C = 64) keep every lane busy.
-template <int MODE>
+// with g = dy masked by y > 0 when relu (and written to dres when given).  A block is TC lanes of V
+// channels x (256 / TC) row lanes (TC = min(C / V, 256) rounded to a power of two), reduced in
+// LDS, so narrow layers (C = 64) keep every lane busy.  V = 4 when C % 4 == 0 and the operands
+// are 16-byte aligned.
+template <int MODE, int V>
 __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restrict__ a, const float* __restrict__ dy,
                                                           const float* __restrict__ y, int relu, long long P, int C,
                                                           int tc, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, float* __restrict__ dres,
                                                           int chunks, double* __restrict__ part) {
-  __shared__ double red[2][256];
+  __shared__ double red[2 * V][256];
   const int chunk = blockIdx.y;
   const long long rows = (P + chunks - 1) / chunks;
   const long long r0 = chunk * rows, r1 = min(P, r0 + rows);
   const int lc = threadIdx.x % tc, lr = threadIdx.x / tc, nr = blockDim.x / tc;
-  const int c = blockIdx.x * tc + lc;
-  double s0 = 0.0, s1 = 0.0;
+  const int c = (blockIdx.x * tc + lc) * V;
+  double s0[V], s1[V];
+  for (int j = 0; j < V; ++j) s0[j] = s1[j] = 0.0;
   if (c < C) {
     if (MODE == 0) {
       for (long long r = r0 + lr; r < r1; r += nr) {
-        const double v = a[r * C + c];
-        s0 += v;
-        s1 += v * v;
+        float v[V];
+        ldv<V>(a, r * C + c, v);
+        for (int j = 0; j < V; ++j) {
+          s0[j] += (double)v[j];
+          s1[j] += (double)v[j] * (double)v[j];
+        }
       }
     } else {
-      const float m = mean[c], is = invstd[c];
+      float m[V], is[V];
+      ldv<V>(mean, c, m);
+      ldv<V>(invstd, c, is);
       for (long long r = r0 + lr; r < r1; r += nr) {
-        float g = dy[r * C + c];
-        if (relu && !(y[r * C + c] > 0.f)) g = 0.f;
-        if (dres) dres[r * C + c] = g;
-        s0 += g;
-        s1 += (double)g * (double)((a[r * C + c] - m) * is);
+        float g[V], yy[V], x[V];
+        ldv<V>(dy, r * C + c, g);
+        ldv<V>(a, r * C + c, x);
+        if (relu) {
+          ldv<V>(y, r * C + c, yy);
+          for (int j = 0; j < V; ++j)
+            if (!(yy[j] > 0.f)) g[j] = 0.f;
+        }
+        if (dres) stv<V>(dres, r * C + c, g);
+        for (int j = 0; j < V; ++j) {
+          s0[j] += g[j];
+          s1[j] += (double)g[j] * (double)((x[j] - m[j]) * is[j]);
+        }
       }
     }
   }
-  red[0][threadIdx.x] = s0;
-  red[1][threadIdx.x] = s1;
+  for (int j = 0; j < V; ++j) {
+    red[2 * j][threadIdx.x] = s0[j];
+    red[2 * j + 1][threadIdx.x] = s1[j];
+  }
   __syncthreads();
   if (lr == 0 && c < C) {
-    for (int k = 1; k < nr; ++k) {
-      s0 += red[0][k * tc + lc];
-      s1 += red[1][k * tc + lc];
+    for (int k = 1; k < nr; ++k)
+      for (int j = 0; j < V; ++j) {
+        s0[j] += red[2 * j][k * tc + lc];
+        s1[j] += red[2 * j + 1][k * tc + lc];
+      }
+    for (int j = 0; j < V; ++j) {
+      part[(long long)chunk * 2 * C + c + j] = s0[j];
+      part[(long long)chunk * 2 * C + C + c + j] = s1[j];
     }
-    part[(long long)chunk * 2 * C + c] = s0;
-    part[(long long)chunk * 2 * C + C + c] = s1;
   }
 }
 
@@ -130,8 +169,8 @@ int bn_lanes(int C) {
 }
 
 // row chunks of the two-stage reductions: enough blocks to fill the chip, at least 4 rows per lane
-int bn_chunks(long long P, int C) {
-  const int tc = bn_lanes(C), nr = 256 / tc, cblocks = (C + tc - 1) / tc;
+int bn_chunks(long long P, int C, int V) {
+  const int tc = bn_lanes(C / V), nr = 256 / tc, cblocks = (C / V + tc - 1) / tc;
   long long k = (2048 + cblocks - 1) / cblocks;
   k = std::min<long long>(k, std::max<long long>(1, P / (4LL * nr)));
   return (int)std::max<long long>(1, std::min<long long>(k, BN_CHUNKS));
@@ -530,7 +569,7 @@ static int splitk_slices(int m, int n, int k) {
   const long long tiles = (long long)((m + 63) / 64) * ((n + 255) / 256);
   const long long target = env_switch("EOSV_SPLITK_TARGET", 256);
   long long s = (target + tiles - 1) / tiles;
-  s = std::min<long long>(s, std::max(1, k / env_switch("EOSV_SPLITK_MINROWS", 1024)));
+  s = std::min<long long>(s, std::max(1, k / env_switch("EOSV_SPLITK_MINROWS", 2048)));
   return (int)std::max<long long>(1, std::min<long long>(s, 256));
 }
 
@@ -607,9 +646,15 @@ int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gam
     return set_error("eosv_bn_train_forward: bad argument"), EOSV_ERR_ARG;
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
-  const int tc = bn_lanes(C), chunks = bn_chunks(P, C);
-  hipLaunchKernelGGL((bn_partials_kernel<0>), dim3((C + tc - 1) / tc, chunks), dim3(256), 0, s, d_x, nullptr, nullptr,
-                     0, (long long)P, C, tc, nullptr, nullptr, nullptr, chunks, part);
+  const int V = C % 4 == 0 && al16(d_x) ? 4 : 1;
+  const int tc = bn_lanes(C / V), chunks = bn_chunks(P, C, V);
+  const dim3 pg((C / V + tc - 1) / tc, chunks);
+  if (V == 4)
+    hipLaunchKernelGGL((bn_partials_kernel<0, 4>), pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc,
+                       nullptr, nullptr, nullptr, chunks, part);
+  else
+    hipLaunchKernelGGL((bn_partials_kernel<0, 1>), pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc,
+                       nullptr, nullptr, nullptr, chunks, part);
   hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3((C + 15) / 16), dim3(256), 0, s, part, chunks, (long long)P, C, eps,
                      momentum, d_running_mean, d_running_var, d_save_mean, d_save_invstd, nullptr);
   if (C % 4 == 0 && al16(d_x) && al16(d_y) && al16(d_residual) && al16(d_save_mean) && al16(d_save_invstd) &&
@@ -633,9 +678,18 @@ int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const 
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
   double* sums = part + (long long)2 * BN_CHUNKS * C;
-  const int tc = bn_lanes(C), chunks = bn_chunks(P, C);
-  hipLaunchKernelGGL((bn_partials_kernel<1>), dim3((C + tc - 1) / tc, chunks), dim3(256), 0, s, d_x, d_dy, d_y, relu,
-                     (long long)P, C, tc, d_save_mean, d_save_invstd, d_dres, chunks, part);
+  const int V = C % 4 == 0 && al16(d_x) && al16(d_dy) && al16(d_y) && al16(d_dres) && al16(d_save_mean) &&
+                        al16(d_save_invstd)
+                    ? 4
+                    : 1;
+  const int tc = bn_lanes(C / V), chunks = bn_chunks(P, C, V);
+  const dim3 pg((C / V + tc - 1) / tc, chunks);
+  if (V == 4)
+    hipLaunchKernelGGL((bn_partials_kernel<1, 4>), pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc,
+                       d_save_mean, d_save_invstd, d_dres, chunks, part);
+  else
+    hipLaunchKernelGGL((bn_partials_kernel<1, 1>), pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc,
+                       d_save_mean, d_save_invstd, d_dres, chunks, part);
   hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3((C + 15) / 16), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f,
                      0.f, nullptr, nullptr, d_dgamma, d_dbeta, sums);
   if (C % 4 == 0 && al16(d_dy) && al16(d_y) && al16(d_x) && al16(d_dx) && al16(d_gamma) && al16(d_save_mean) &&

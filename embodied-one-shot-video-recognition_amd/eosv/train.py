@@ -194,8 +194,9 @@ class NativeTrainer:
             check(rc, "eosv_conv2d_f32")
         return y, (N, Ho, Wo, c.cout)
 
-    def _conv_bwd(self, dz, x, shape, c: _Conv, s, need_dx=True):
-        """dW = dz^T . col(x); returns dx = col2im(dz . W) (NHWC, shape of x) when need_dx."""
+    def _conv_bwd(self, dz, x, shape, c: _Conv, s, need_dx=True, acc=None):
+        """dW = dz^T . col(x); returns dx = col2im(dz . W) (NHWC, shape of x) when need_dx, plus
+        acc (same shape) when given -- fused into the conv epilogue on the fast path."""
         N, H, W, _ = shape
         Ho, Wo = (H + 2 * c.pad - c.k) // c.stride + 1, (W + 2 * c.pad - c.k) // c.stride + 1
         P = N * Ho * Wo
@@ -216,8 +217,8 @@ class NativeTrainer:
             # stride 1: dx = conv(dz, W flipped and transposed) on the inference conv kernels
             wf = self._buf("wflip", c.cout * c.K)
             check(self.L.eosv_flip_weights(_f(c.w), c.cout, c.k, c.k, c.cin, _f(wf), s), "eosv_flip_weights")
-            rc = self.L.eosv_conv2d_f32(_f(dz), N, Ho, Wo, c.cout, _f(wf), c.cin, c.k, c.k, 1, c.pad, None, None, 0,
-                                        _f(dx), s)
+            rc = self.L.eosv_conv2d_f32(_f(dz), N, Ho, Wo, c.cout, _f(wf), c.cin, c.k, c.k, 1, c.pad, None, _f(acc),
+                                        0, _f(dx), s)
             if rc != _UNSUPPORTED:
                 check(rc, "eosv_conv2d_f32")
                 return dx
@@ -226,6 +227,8 @@ class NativeTrainer:
               "eosv_sgemm")
         if not direct:
             check(self.L.eosv_col2im(_f(dcol), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(dx), s), "eosv_col2im")
+        if acc is not None:
+            check(self.L.eosv_axpy(_f(dx), _f(acc), dx.numel(), 1.0, s), "eosv_axpy")
         return dx
 
     def _bn_fwd(self, z, P, b: _BN, relu, res, s):
@@ -329,14 +332,16 @@ class NativeTrainer:
                 dz, dr = self._bn_bwd(g, sv["y"][i], True, sv["z"][i], P, b, st, s, want_dres=(i == nl - 1))
                 if i == nl - 1:
                     dres = dr
-                g = self._conv_bwd(dz, sv["in"][i], sv["inshape"][i], c, s, need_dx=True)
-            if blk.ds is not None:
-                zd, sc, std, Pd = sv["ds"]
-                dzd, _ = self._bn_bwd(dres, None, False, zd, Pd, blk.ds_bn, std, s)
-                gd = self._conv_bwd(dzd, sv["x"], sv["shape"], blk.ds, s, need_dx=True)
-                check(L.eosv_axpy(_f(g), _f(gd), g.numel(), 1.0, s), "eosv_axpy")
-            else:
-                check(L.eosv_axpy(_f(g), _f(dres), g.numel(), 1.0, s), "eosv_axpy")
+                skip = None
+                if i == 0:
+                    # the block input's gradient through the shortcut, added to the first conv's dx
+                    if blk.ds is not None:
+                        zd, sc, std, Pd = sv["ds"]
+                        dzd, _ = self._bn_bwd(dres, None, False, zd, Pd, blk.ds_bn, std, s)
+                        skip = self._conv_bwd(dzd, sv["x"], sv["shape"], blk.ds, s, need_dx=True)
+                    else:
+                        skip = dres
+                g = self._conv_bwd(dz, sv["in"][i], sv["inshape"][i], c, s, need_dx=True, acc=skip)
             dh = g
             blk.saved = {}
         da0 = torch.empty(P1 * 64, dtype=torch.float32, device=self.dev)

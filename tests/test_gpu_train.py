@@ -198,6 +198,12 @@ def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
         _call(L.eosv_conv2d_f32, dyd.data_ptr(), N, Ho, Wo, cout, wf.data_ptr(), cin, k, k, 1, pad, None, None, 0,
               gx.data_ptr())
         assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad) < 1e-5
+        # the shortcut's gradient fused as the epilogue residual (the trainer's first-conv dgrad)
+        sk = torch.randn(N, H, H, cin, dtype=torch.float64)
+        skd = sk.float().cuda().contiguous()
+        _call(L.eosv_conv2d_f32, dyd.data_ptr(), N, Ho, Wo, cout, wf.data_ptr(), cin, k, k, 1, pad, None,
+              skd.data_ptr(), 0, gx.data_ptr())
+        assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad + sk.permute(0, 3, 1, 2)) < 1e-5
 
 
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
