@@ -100,6 +100,8 @@ def _install_stubs():
 
     class ToTensor:
         def __call__(self, img):
+            if FRAME_LOG is not None:
+                FRAME_LOG.append((img.video_info, img.fid))
             cls = img.video_info.split("/")[0]
             return torch.from_numpy(synth.synth_frame(cls, img.video_info, img.fid, SHAPE["H"], SHAPE["W"]))
 
@@ -123,6 +125,7 @@ def _install_stubs():
 
 
 FRAME_DIR = None
+FRAME_LOG = None  # (video_info, frame id) of every frame the ToTensor stub makes, when a list
 
 
 def _import_reference(gallery_path):
@@ -133,6 +136,7 @@ def _import_reference(gallery_path):
     FRAME_DIR = utils.KINETICS_FRAME_DIR
     fake_os = types.ModuleType("os_stub")
     fake_os.path = os.path
+    fake_os.makedirs = os.makedirs  # network_train.py:36 (its `os` is utils' through the star import)
     fake_os.listdir = lambda p: [None] * (synth.frame_count(os.path.relpath(p, FRAME_DIR)) + 1)
     utils.os = fake_os
     fake_image = types.ModuleType("Image_stub")
@@ -488,6 +492,127 @@ def capture_layer_checksums(mods, tag, archs=("resnet18", "resnet50")):
     print(tag, {k: [round(st["sum"], 3) for st in v] for k, v in out["archs"].items()})
 
 
+def _tensor_stats(t, i):
+    """Size-independent summary of one state_dict tensor (its i-th): sum, norm and the projection
+    onto a fixed N(0,1) tensor (numpy default_rng(2000 + i))."""
+    a = t.detach().double().numpy().reshape(-1)
+    r = np.random.default_rng(2000 + i).standard_normal(a.shape)
+    return dict(sum=float(a.sum()), norm=float(np.sqrt((a * a).sum())), proj=float((a * r).sum()))
+
+
+def _projections(t, i, n=8):
+    """n projections of tensor i onto N(0,1) tensors (numpy default_rng(3000 + 8 i + j)): for a
+    difference d of two updates, their RMS estimates |d| (E (r.d)^2 = |d|^2)."""
+    a = t.detach().double().numpy().reshape(-1)
+    return [float((a * np.random.default_rng(3000 + 8 * i + j).standard_normal(a.shape)).sum()) for j in range(n)]
+
+
+def capture_train(mods, arch_name, tag, T=8, res=96, batch=2, epochs=2, step_size=1, lr1=1e-3, lr2=1e-2,
+                  n_classes=3, per_class=2, seed=0):
+    """the reference's own TrainNetwork.finetune_model (network_train.py:21-131)
+    over a tiny train list (the first ``per_class`` videos of the first ``n_classes`` classes of
+    its sources/data/train.list whose synthetic length holds a T-frame clip), ``epochs`` epochs
+    with StepLR(step_size) so the schedule's first decay is exercised, from the synthetic
+    state_dict of seed 0.
+
+    Patches beyond the inference stubs, each the minimum this torch needs: the DataLoader runs
+    without workers (network_train.py:66 asks for 8; the batches are recorded either way), the
+    loss returned by CrossEntropyLoss is reshaped to [1] so that ``loss.data[0]``
+    (network_train.py:125, PyTorch 0.3 indexing) works, and the loaders' bound ``video_frames``
+    default is set to T (as the shape helper does).  Recorded: every batch (video ids, clip start
+    frame, labels), every iteration's loss, and per-epoch statistics of every state_dict tensor
+    (from the reference's own checkpoints, network_train.py:130-131)."""
+    global FRAME_LOG
+    u = mods["utils"]
+    lines = [l.strip() for l in open(os.path.join(REF, "sources/data/train.list")) if l.strip()]
+    pick, per = [], {}
+    for l in lines:
+        c = l.split("/")[0]
+        if c not in per and len(per) == n_classes:
+            break
+        if per.get(c, 0) < per_class and synth.frame_count(l) >= T + 3:
+            pick.append(l)
+            per[c] = per.get(c, 0) + 1
+    tmpd = tempfile.mkdtemp()
+    tl = os.path.join(tmpd, "train.list")
+    with open(tl, "w") as f:
+        f.write("\n".join(pick) + "\n")
+    import epoch_dataloader as edl_t
+    import network_train as ntr
+    ntr.TRAIN_LIST = tl
+    old_defaults = u.get_video_from_video_info.__defaults__
+    u.get_video_from_video_info.__defaults__ = (T,) + old_defaults[1:]
+    SHAPE["H"] = SHAPE["W"] = res
+    dl0 = ntr.DataLoader
+    ntr.DataLoader = lambda ds, **k: dl0(ds, **{**k, "num_workers": 0})
+    losses, labels = [], []
+
+    class CE(torch.nn.CrossEntropyLoss):
+        def forward(self, out, lab):
+            loss = super().forward(out, lab)
+            losses.append(float(loss.detach()))
+            labels.append([int(v) for v in lab])
+            return loss.reshape(1)
+
+    nn_stub = types.ModuleType("nn")
+    nn_stub.__dict__.update(torch.nn.__dict__)
+    nn_stub.CrossEntropyLoss = CE
+    ntr.nn = nn_stub
+    clips = []
+    gi0 = edl_t.VideoDataset.__getitem__
+
+    def getitem(self, idx):
+        n0 = len(FRAME_LOG)
+        out = gi0(self, idx)
+        fr = FRAME_LOG[n0:]
+        clips.append(dict(video=fr[0][0], start=int(fr[0][1]), n=len(fr)))
+        return out
+
+    edl_t.VideoDataset.__getitem__ = getitem
+    sd_path = os.path.join(tmpd, "init.pkl")
+    _save_state_dict(arch_name, sd_path)
+    sd0 = torch.load(sd_path, weights_only=True)
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    FRAME_LOG = []
+    ckp = os.path.join(tmpd, "ckp") + "/"
+    try:
+        tn = ntr.TrainNetwork(os.path.join(tmpd, "loss.txt"), ckp, epochs, batch, lr1, lr2, step_size, arch_name)
+        clips.clear()
+        FRAME_LOG.clear()
+        tn.finetune_model(data_aug="None", pre_model=sd_path)
+    finally:
+        FRAME_LOG = None
+        edl_t.VideoDataset.__getitem__ = gi0
+        ntr.DataLoader = dl0
+        u.get_video_from_video_info.__defaults__ = old_defaults
+        SHAPE["H"] = SHAPE["W"] = H
+    per_epoch = len(losses) // epochs
+    it = 0
+    meta = dict(arch=arch_name, T=T, H=res, W=res, batch=batch, epochs=epochs, step_size=step_size, lr_1=lr1,
+                lr_2=lr2, num_classes=64, init_seed=0, train_list=pick, epochs_data=[])
+    for e in range(epochs):
+        its = []
+        for _ in range(per_epoch):
+            its.append(dict(clips=clips[it * batch:(it + 1) * batch], labels=labels[it], loss=losses[it]))
+            it += 1
+        sd = torch.load(ckp + f"model{e + 1}.pkl", weights_only=True)
+        stats = {}
+        for i, (k, v) in enumerate(sd.items()):
+            if k.endswith("num_batches_tracked"):
+                stats[k] = int(v)
+                continue
+            dv = v.double() - sd0[k].double()  # the update since the start
+            d = _tensor_stats(dv, i)
+            stats[k] = dict(_tensor_stats(v, i), dsum=d["sum"], dnorm=d["norm"], dproj=d["proj"],
+                            dproj8=_projections(dv, i))
+        meta["epochs_data"].append(dict(iterations=its, state=stats))
+    with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(tag, "losses", [round(l, 6) for l in losses])
+
+
 def make_unreal14_list(path):
     """An UnrealAction-shaped novel split (README.md:23-26: 14 actions, 10 real target videos
     each), in the reference's ``class/video`` list format; names are synthetic."""
@@ -506,6 +631,7 @@ def main():
     ap.add_argument("--layers", action="store_true", help="only the one-frame per-layer checksums")
     ap.add_argument("--svm", action="store_true", help="only the SVM-classifier baseline episodes")
     ap.add_argument("--aug-seed6", action="store_true", help="only the 8-episode config-3 fixture")
+    ap.add_argument("--train", action="store_true", help="only the training-loop fixtures (R18, R50)")
     args = ap.parse_args()
     torch.set_num_threads(8)
     _install_stubs()
@@ -513,6 +639,10 @@ def main():
     mods = _import_reference(gallery_path)
     if args.layers:
         capture_layer_checksums(mods, "layers_one_frame")
+        return
+    if args.train:
+        capture_train(mods, "resnet18", "train_r18_t8_96")
+        capture_train(mods, "resnet50", "train_r50_t8_96")
         return
     if args.svm:
         capture_baseline(mods, "resnet18", "SVM", seed=5, episodes=8, tag="c1_r18_svm_seed5")

@@ -342,3 +342,53 @@ def test_dropin_train_network_checkpoints_follow_reference(tmp_path, monkeypatch
         err = float((got[k].double() - v).norm())
         yard = float((f32[k].double() - v).norm())
         assert err <= max(4 * yard, 1e-6 * v.numel() ** 0.5 + 1e-5 * float(v.norm())), (k, err, yard)
+
+
+@pytest.mark.parametrize("tag", ["train_r18_t8_96", "train_r50_t8_96"])
+def test_train_loop_matches_reference_fixture(tag, golden_dir):
+    """The native step replayed over the batches the reference's own finetune_model consumed
+    (tests/golden/train_*.json, capture_golden.py --train: 2 epochs x 3 batches of 2 clips x 8
+    frames at 96x96, StepLR(1) so the second epoch runs at the decayed rate), with the drop-in
+    TrainNetwork's schedule.  Truth: the restated loop (oracle/train_ref.py, bit-identical to the
+    reference in f32 -- tests/test_oracle_golden.py) run in f64; yardstick: the reference's own f32
+    run.  Every loss within max(4 x the reference's distance, 1e-4 relative); every checkpoint
+    tensor's update (final - initial) within max(4 x the reference's distance, 2e-2 of the
+    update's norm), distances as norms (the reference's estimated from the fixture's 8 random
+    projections of its update: E (r.d)^2 = |d|^2); num_batches_tracked equal."""
+    import json
+    import os
+    import types
+
+    from network_train import TrainNetwork
+    from oracle import train_ref
+
+    meta = json.load(open(os.path.join(golden_dir, tag + ".json")))
+    sd0 = synth.synth_state_dict(arch.SPECS[meta["arch"]], meta["num_classes"], meta["init_seed"])
+    truth_losses, truth_states = train_ref.train_replay(meta, sd0, torch.float64)
+    tr = NativeTrainer(meta["arch"], meta["num_classes"], device=0)
+    tr.load_state_dict(sd0)
+    sched = types.SimpleNamespace(lr_1=meta["lr_1"], lr_2=meta["lr_2"], lr_step_size=meta["step_size"])
+    k, worst = 0, 0.0
+    for e, ep in enumerate(meta["epochs_data"]):
+        lr1, lr2 = TrainNetwork.lr_at(sched, e)
+        for it in ep["iterations"]:
+            frames = train_ref.batch_frames(it, meta["H"], meta["W"])
+            loss, _ = tr.step(frames.cuda(), it["labels"], meta["T"], lr1, lr2)
+            t = truth_losses[k]
+            assert abs(loss - t) <= max(4 * abs(it["loss"] - t), 1e-4 * abs(t)), (e, k, loss, t, it["loss"])
+            k += 1
+        got = tr.state_dict()
+        for i, key in enumerate(ep["state"]):
+            st = ep["state"][key]
+            if key.endswith("num_batches_tracked"):
+                assert int(got[key]) == st, key
+                continue
+            init = torch.as_tensor(np.asarray(sd0[key])).double()
+            d_truth = truth_states[e][key].double() - init
+            p_truth = np.asarray(train_ref.projections(d_truth, i))
+            yard = float(np.sqrt(np.mean((np.asarray(st["dproj8"]) - p_truth) ** 2)))
+            tn = float(d_truth.norm())
+            err = float((got[key].double() - init - d_truth).norm())
+            worst = max(worst, err / max(tn, 1e-30))
+            assert err <= max(4 * yard, 2e-2 * tn) + 1e-12, (e, key, err, yard, tn)
+    print(f"[{tag}] worst update error {worst:.2e} of the update's norm")

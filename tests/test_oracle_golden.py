@@ -3,6 +3,8 @@
 Fixtures come from tests/golden/capture_golden.py, which ran the reference's own
 EpisodeDataloader / TestNetwork / Classifier code in the build container.
 """
+import json
+import os
 import random
 
 import numpy as np
@@ -61,3 +63,35 @@ def test_oracle_harness_matches_reference(tag):
         assert np.array_equal(r["pred"], arr["pred"][i])
     accs = [r["acc"] for r in res]
     assert "\n".join(harness_ref.acc_lines(accs)) + "\n" == meta["acc_file"]
+
+
+@pytest.mark.parametrize("tag", ["train_r18_t8_96", "train_r50_t8_96"])
+def test_training_oracle_matches_reference_loop(tag, golden_dir):
+    """oracle/train_ref.py (the restated finetune_model loop) in f32 on the CPU against the
+    reference's own loop on the same batches (capture_golden.py --train): every iteration's loss
+    and every epoch checkpoint's update (projection of final - initial, per tensor)."""
+
+    from oracle import train_ref
+
+    meta = json.load(open(os.path.join(golden_dir, tag + ".json")))
+    sd0 = synth.synth_state_dict(arch.SPECS[meta["arch"]], meta["num_classes"], meta["init_seed"])
+    nt = torch.get_num_threads()
+    torch.set_num_threads(8)  # the capture's thread count: same oneDNN blocking, same sums
+    try:
+        losses, states = train_ref.train_replay(meta, sd0, torch.float32)
+    finally:
+        torch.set_num_threads(nt)
+    ref = [it["loss"] for ep in meta["epochs_data"] for it in ep["iterations"]]
+    for a, b in zip(losses, ref):
+        assert abs(a - b) <= 1e-6 * abs(b), (a, b)
+    for e, ep in enumerate(meta["epochs_data"]):
+        for i, (k, v) in enumerate(states[e].items()):
+            st = ep["state"][k]
+            if k.endswith("num_batches_tracked"):
+                assert int(v) == st, k
+                continue
+            d = train_ref.tensor_stats(v.double() - torch.as_tensor(np.asarray(sd0[k])).double(), i)
+            assert abs(d["proj"] - st["dproj"]) <= 1e-3 * st["dnorm"] + 1e-12, (e, k, d, st)
+            assert abs(d["norm"] - st["dnorm"]) <= 1e-3 * st["dnorm"] + 1e-12, (e, k, d, st)
+            p8 = train_ref.projections(v.double() - torch.as_tensor(np.asarray(sd0[k])).double(), i)
+            assert np.allclose(p8, st["dproj8"], rtol=0, atol=1e-3 * st["dnorm"] + 1e-12), (e, k)
