@@ -312,7 +312,8 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
 }
 
 // Tile per layer (r01 / r01l A/B): 256x64 (4 waves of 64x64) for Cout 64, 256x128
-// (8 waves) for Cout 128 / 256, 128x128 for Cout >= 512, all BK 16 with a 2-deep ring.  The fc
+// (8 waves) for Cout 128 / 256, 128x128 for Cout >= 512, all BK 16 with a 2-deep ring; 128x128 /
+// 128x64 when the grid would not cover the CUs (small batches).  The fc
 // head (M = frames, Cout = num_classes) runs here too: when Cout % 4 != 0 its rows are not 16-B
 // aligned, so it takes the per-element epilogue instead of the LDS-staged float4 one.
 int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
@@ -343,8 +344,13 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
   if (tile == 5) return launch_dma<512, 128, 16, 4, 2, false>(a, s);  // 8 waves of 128x64
   if (tile == 6 && a.Cout <= 256) return launch_dma<512, 128, 16, 4, 2, false>(a, s);
 #endif
-  if (a.Cout <= 256) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
-  return launch_dma<128, 128, 16, 2, 2, false>(a, s);
+  // small batches (the training step: 96 frames): a grid below the chip's CU count leaves
+  // CUs idle, so the tile shrinks (same BK, same k-order per output: bit-identical results)
+  const long long M = (long long)a.N * a.Ho * a.Wo, cus = device_cu_count();
+  auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
+  if (a.Cout <= 256 && blocks(256, 128) >= cus) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
+  if (blocks(128, 128) >= cus) return launch_dma<128, 128, 16, 2, 2, false>(a, s);
+  return launch_dma<128, 64, 16, 2, 2, false>(a, s);
 }
 
 }  // namespace eosv

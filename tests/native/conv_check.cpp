@@ -479,6 +479,9 @@ int main() {
   fails += check(6, 14, 14, 256, 256, 3, 1, 1, false, true, true, 0, 2e-6);
   fails += check(4, 14, 14, 256, 256, 3, 1, 1, false, false, true, 128, 2e-6);
   fails += check(3, 7, 7, 512, 512, 3, 1, 1, false, false, true, 256, 2e-6);
+  // grids at / above the CU count: the large 256x128 and 128x128 tiles (small N takes 128x64)
+  fails += check(21, 56, 56, 32, 128, 3, 1, 1, false, true, true, 0, 2e-6);
+  fails += check(11, 28, 28, 32, 512, 1, 1, 0, false, false, true, 0, 2e-6);
   fails += check(3, 9, 11, 32, 64, 3, 1, 1, false, true, false, 0, 2e-6);
   fails += check(2, 5, 3, 32, 128, 3, 1, 1, false, true, true, 32, 2e-6);
   printf("%d failures\n", fails);
