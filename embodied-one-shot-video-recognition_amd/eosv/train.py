@@ -201,15 +201,25 @@ class NativeTrainer:
         Ho, Wo = (H + 2 * c.pad - c.k) // c.stride + 1, (W + 2 * c.pad - c.k) // c.stride + 1
         P = N * Ho * Wo
         direct = c.k == 1 and c.stride == 1
-        if direct:
-            col = x
+        rc = _UNSUPPORTED
+        if c.k > 1:
+            # KxK: implicit-GEMM weight gradient (no im2col buffer)
+            wb = int(self.L.eosv_conv_wgrad_f32_workspace(N, H, W, c.cin, c.cout, c.k, c.k, c.stride, c.pad))
+            ws = self._buf("splitk", wb // 4 + 4)
+            rc = self.L.eosv_conv_wgrad_f32(_f(x), N, H, W, c.cin, _f(dz), c.cout, c.k, c.k, c.stride, c.pad, _f(c.g),
+                                            _f(ws), wb, s)
+        if rc == _UNSUPPORTED:
+            if direct:
+                col = x
+            else:
+                col = self._buf("col", P * c.K)
+                check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
+            wb = int(self.L.eosv_sgemm_tn_splitk_workspace(c.cout, c.K, P))
+            ws = self._buf("splitk", wb // 4 + 1)
+            check(self.L.eosv_sgemm_tn_splitk(c.cout, c.K, P, _f(dz), c.cout, _f(col), c.K, _f(c.g), c.K, _f(ws), wb,
+                                              s), "eosv_sgemm_tn_splitk")
         else:
-            col = self._buf("col", P * c.K)
-            check(self.L.eosv_im2col(_f(x), N, H, W, c.cin, c.k, c.k, c.stride, c.pad, _f(col), s), "eosv_im2col")
-        wb = int(self.L.eosv_sgemm_tn_splitk_workspace(c.cout, c.K, P))
-        ws = self._buf("splitk", wb // 4 + 1)
-        check(self.L.eosv_sgemm_tn_splitk(c.cout, c.K, P, _f(dz), c.cout, _f(col), c.K, _f(c.g), c.K, _f(ws), wb, s),
-              "eosv_sgemm_tn_splitk")
+            check(rc, "eosv_conv_wgrad_f32")
         if not need_dx:
             return None
         dx = torch.empty(N * H * W * c.cin, dtype=torch.float32, device=self.dev)

@@ -197,6 +197,14 @@ int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const
 int64_t eosv_sgemm_tn_splitk_workspace(int m, int n, int k);
 int eosv_sgemm_tn_splitk(int m, int n, int k, const float* d_a, int lda, const float* d_b, int ldb, float* d_c,
                          int ldc, float* d_work, int64_t work_bytes, eosv_stream_t stream);
+/* Weight gradient of a KxK conv without the im2col buffer: dW[Cout][KH][KW][Cin] = sum over
+ * output pixels of dY[p][co] * X[in(p, kh, kw)][ci] (NHWC x [N][H][W][Cin], dY [P][Cout]), an
+ * implicit GEMM on exact-f32 MFMA with the pixel reduction split into slices summed in order
+ * (deterministic).  EOSV_ERR_UNSUPPORTED unless Cin % 4 == 0 and (Cout % 128, K % 128) or
+ * (Cout % 64, K % 192), K = KH KW Cin; d_work: eosv_conv_wgrad_f32_workspace(...) bytes. */
+int64_t eosv_conv_wgrad_f32_workspace(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
+int eosv_conv_wgrad_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_dy, int Cout, int KH, int KW,
+                        int stride, int pad, float* d_dw, float* d_work, int64_t work_bytes, eosv_stream_t stream);
 /* im2col of NHWC x: col[(n, oh, ow)][(kh, kw, c)], zero padding; col2im is its adjoint
  * (gather-sum, overwrites d_x). */
 int eosv_im2col(const float* d_x, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_col,
