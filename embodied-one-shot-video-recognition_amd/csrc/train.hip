@@ -176,19 +176,19 @@ int bn_chunks(long long P, int C, int V) {
   return (int)std::max<long long>(1, std::min<long long>(k, BN_CHUNKS));
 }
 
-// the second stage: 16 channel lanes x 16 chunk lanes per block (fixed order, deterministic), then
+// the second stage: 8 channel lanes x 32 chunk lanes per block (fixed order, deterministic), then
 // MODE 0 the batch statistics and running estimates, MODE 1 dgamma / dbeta and the sums for dx
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int chunks, long long P,
                                                           int C, float eps, float momentum, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, float* __restrict__ out0,
                                                           float* __restrict__ out1, double* __restrict__ sums) {
-  __shared__ double red[2][16][17];
-  const int lc = threadIdx.x & 15, lk = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + lc;
+  __shared__ double red[2][32][9];
+  const int lc = threadIdx.x & 7, lk = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + lc;
   double s0 = 0.0, s1 = 0.0;
   if (c < C)
-    for (int k = lk; k < chunks; k += 16) {
+    for (int k = lk; k < chunks; k += 32) {
       s0 += part[(long long)k * 2 * C + c];
       s1 += part[(long long)k * 2 * C + C + c];
     }
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
   red[1][lk][lc] = s1;
   __syncthreads();
   if (lk != 0 || c >= C) return;
-  for (int j = 1; j < 16; ++j) {
+  for (int j = 1; j < 32; ++j) {
     s0 += red[0][j][lc];
     s1 += red[1][j][lc];
   }
@@ -655,7 +655,7 @@ int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gam
   else
     hipLaunchKernelGGL((bn_partials_kernel<0, 1>), pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc,
                        nullptr, nullptr, nullptr, chunks, part);
-  hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3((C + 15) / 16), dim3(256), 0, s, part, chunks, (long long)P, C, eps,
+  hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, eps,
                      momentum, d_running_mean, d_running_var, d_save_mean, d_save_invstd, nullptr);
   if (C % 4 == 0 && al16(d_x) && al16(d_y) && al16(d_residual) && al16(d_save_mean) && al16(d_save_invstd) &&
       al16(d_gamma) && al16(d_beta))
@@ -690,7 +690,7 @@ int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const 
   else
     hipLaunchKernelGGL((bn_partials_kernel<1, 1>), pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc,
                        d_save_mean, d_save_invstd, d_dres, chunks, part);
-  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3((C + 15) / 16), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f,
+  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f,
                      0.f, nullptr, nullptr, d_dgamma, d_dbeta, sums);
   if (C % 4 == 0 && al16(d_dy) && al16(d_y) && al16(d_x) && al16(d_dx) && al16(d_gamma) && al16(d_save_mean) &&
       al16(d_save_invstd))
