@@ -89,6 +89,11 @@ struct ConvArgs {
   // (0 = derive; conv_pixel_strides)
   int xs, x2s;
   LaunchInfo* plan;   // host-side: non-null = record the grid (record_launch), launch nothing
+  // f32 implicit GEMM only (the training entry eosv_conv2d_f32): split the K loop over
+  // gridDim.y = ksplit slices writing raw partial sums to kws ([ksplit][M][Cout]); the launcher
+  // then sums them in slice order with the bias / residual / ReLU epilogue.  0 / 1 = off.
+  int ksplit;
+  float* kws;
 };
 
 __host__ __device__ inline int split_chan(int c, int cin3) {

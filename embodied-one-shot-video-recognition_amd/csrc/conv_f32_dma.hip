@@ -24,6 +24,8 @@
 // (tests/native/dma_probe.cpp).  No bounds checks: the borders are real zeros.
 #include "common.h"
 
+#include <algorithm>
+
 namespace eosv {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -164,9 +166,18 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   const int h = lane >> 5;
   const int r = lane & 31;
   const int sw = (r / RPB) & (CPR - 1);
-  const int nk = a.K / BK;
+  // K-step range: all of K, or slice blockIdx.y of gridDim.y (split-K, raw partials)
+  const int nkt = a.K / BK;
+  const int kb = (int)((long long)nkt * blockIdx.y / gridDim.y);
+  const int nk = (int)((long long)nkt * (blockIdx.y + 1) / gridDim.y) - kb;
+  if (kb > 0 && !STEM) {  // the tap counters of K column kb * BK
+    const int k = kb * BK, t = k / a.Cin;
+    nc0 = k - t * a.Cin;
+    nkh = t / a.KW;
+    nkw = t - nkh * a.KW;
+  }
   constexpr int PER = AI + BI;  // DMA instructions per stage per wave
-  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p);
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage((kb + p) * BK, p);
   if (NS == 3 && nk > 1)
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
   else
@@ -176,7 +187,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   int slot = 0, wslot = NS - 1;
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
-    if (issue && !(EOSV_ABL(a) & 1)) stage((kt + NS - 1) * BK, wslot);
+    if (issue && !(EOSV_ABL(a) & 1)) stage((kb + kt + NS - 1) * BK, wslot);
     const float* As = smem + slot * STAGE;
     const float* Bs = As + BM * BK;
 #pragma unroll
@@ -210,13 +221,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
     wslot = wslot + 1 == NS ? 0 : wslot + 1;
   }
 
-  float* __restrict__ y = (float*)a.y;
-  const float* __restrict__ res = (const float*)a.res;
+  const bool part = gridDim.y > 1;  // split-K: raw partial sums, epilogue in the slice sum
+  float* __restrict__ y = part ? a.kws + (long long)blockIdx.y * M * a.Cout : (float*)a.y;
+  const float* __restrict__ res = part ? nullptr : (const float*)a.res;
+  const int relu = part ? 0 : a.relu;
   float bcol[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 32 + r;
-    bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+    bcol[j] = (!part && a.bias && n < a.Cout) ? a.bias[n] : 0.f;
   }
   if constexpr (EPI_LDS) {
     // Epilogue staged through LDS (the ring is free): pass (i, wsel) moves the 32 x BN rows
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
             v.z += rv.z;
             v.w += rv.w;
           }
-          if (a.relu) {
+          if (relu) {
             v.x = fmaxf(v.x, 0.f);
             v.y = fmaxf(v.y, 0.f);
             v.z = fmaxf(v.z, 0.f);
@@ -281,12 +294,44 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
           const long long o = (long long)m * a.Cout + n;
           float v = acc[i][j][q] + bcol[j];
           if (res) v += res[o];
-          if (a.relu) v = fmaxf(v, 0.f);
+          if (relu) v = fmaxf(v, 0.f);
           if (EOSV_ABL(a) & 2) asm volatile("" ::"v"(v)); else y[o] = v;
         }
       }
     }
   }
+}
+
+// split-K epilogue: y = relu(sum over slices (in order) + bias + residual), float4 over Cout
+__global__ void ksplit_sum_kernel(const float4* __restrict__ ws, int ks, long long mc4, int C4,
+                                  const float* __restrict__ bias, const float4* __restrict__ res, int relu,
+                                  float4* __restrict__ y) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < mc4; i += (long long)gridDim.x * blockDim.x) {
+    float4 v = ws[i];
+    for (int z = 1; z < ks; ++z) {
+      const float4 u = ws[z * mc4 + i];
+      v.x += u.x, v.y += u.y, v.z += u.z, v.w += u.w;
+    }
+    if (bias) {
+      const float4 b = reinterpret_cast<const float4*>(bias)[i % C4];
+      v.x += b.x, v.y += b.y, v.z += b.z, v.w += b.w;
+    }
+    if (res) {
+      const float4 q = res[i];
+      v.x += q.x, v.y += q.y, v.z += q.z, v.w += q.w;
+    }
+    if (relu) v.x = fmaxf(v.x, 0.f), v.y = fmaxf(v.y, 0.f), v.z = fmaxf(v.z, 0.f), v.w = fmaxf(v.w, 0.f);
+    y[i] = v;
+  }
+}
+
+static int launch_ksplit_sum(const ConvArgs& a, int ks, long long M, hipStream_t s) {
+  const long long mc4 = M * a.Cout / 4;
+  hipLaunchKernelGGL(ksplit_sum_kernel, dim3((unsigned)std::min<long long>((mc4 + 255) / 256, 1 << 20)), dim3(256), 0,
+                     s, (const float4*)a.kws, ks, mc4, a.Cout / 4, a.bias, (const float4*)a.res, a.relu,
+                     (float4*)a.y);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
 }
 
 template <int BM, int BN, int BK, int WM, int WN, bool STEM, int NS = 2, bool EPI = true>
@@ -299,15 +344,23 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
         (const void*)conv_f32_dma_kernel<BM, BN, BK, WM, WN, false, NS, EPI, false>, 64 * WM * WN);
     return record_launch(a.plan, nb, occ);
   }
+  // split-K (training entry only): enough slices to put ~2 workgroups on every CU, each slice
+  // at least 32 K-steps
+  int ks = 1;
+  if (a.kws && !STEM && !a.x2 && EPI) {
+    const long long want = (2LL * device_cu_count() + nb - 1) / nb;
+    ks = (int)std::max(1LL, std::min({want, (long long)(a.K / BK) / 32, 8LL}));
+  }
   if (a.x2) {
     if (STEM || a.K1 % BK || a.Cin2 % BK) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
     hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, false, NS, EPI, true>), dim3((unsigned)nb),
                        dim3(64 * WM * WN), 0, s, a);
   } else {
-    hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS, EPI, false>), dim3((unsigned)nb),
+    hipLaunchKernelGGL((conv_f32_dma_kernel<BM, BN, BK, WM, WN, STEM, NS, EPI, false>), dim3((unsigned)nb, ks),
                        dim3(64 * WM * WN), 0, s, a);
   }
   EOSV_LAUNCH_CHECK();
+  if (ks > 1) return launch_ksplit_sum(a, ks, M, s);
   return EOSV_OK;
 }
 

@@ -784,9 +784,16 @@ int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_
   return EOSV_OK;
 }
 
+int64_t eosv_conv2d_f32_workspace(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad) {
+  if (N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0) return 0;
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return 0;
+  return (int64_t)8 * N * Ho * Wo * Cout * (int64_t)sizeof(float);  // up to 8 K-slices
+}
+
 int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_w, int Cout, int KH, int KW,
-                    int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y,
-                    eosv_stream_t stream) {
+                    int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y, float* d_work,
+                    int64_t work_bytes, eosv_stream_t stream) {
   if (!d_x || !d_w || !d_y || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || KH <= 0 || KW <= 0 ||
       stride <= 0 || pad < 0)
     return set_error("eosv_conv2d_f32: bad argument"), EOSV_ERR_ARG;
@@ -810,6 +817,10 @@ int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float*
   a.relu = relu;
   a.zero = zero_page(dev);
   a.xcd = 1;
+  // split-K over the workspace when one is given (small grids: the training batch)
+  if (d_work && work_bytes >= eosv_conv2d_f32_workspace(N, H, W, Cin, Cout, KH, KW, stride, pad) &&
+      !((uintptr_t)d_work & 15))
+    a.kws = d_work;
   if (!a.zero) return set_error("eosv_conv2d_f32: zero page allocation failed"), EOSV_ERR_OOM;
   return launch_conv_f32(a, (hipStream_t)stream);
 }

@@ -32,7 +32,7 @@ EXPORTS = ("eosv_create", "eosv_load_weights", "eosv_backbone_forward", "eosv_ba
            "eosv_broadcast_rows", "eosv_softmax_xent", "eosv_sum_rows", "eosv_add_bias", "eosv_sgd_momentum",
            "eosv_axpy", "eosv_nchw_to_nhwc", "eosv_conv2d_f32", "eosv_flip_weights",
            "eosv_sgemm_tn_splitk_workspace", "eosv_sgemm_tn_splitk", "eosv_conv_wgrad_f32_workspace",
-           "eosv_conv_wgrad_f32")
+           "eosv_conv_wgrad_f32", "eosv_conv2d_f32_workspace")
 
 
 class EosvDesc(ctypes.Structure):
@@ -96,7 +96,9 @@ def lib():
         "eosv_sgd_momentum": (i32, [vp, vp, vp, i64, f32, f32, i32, vp]),
         "eosv_axpy": (i32, [vp, vp, i64, f32, vp]),
         "eosv_nchw_to_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
-        "eosv_conv2d_f32": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp]),
+        "eosv_conv2d_f32": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, i64,
+                                  vp]),
+        "eosv_conv2d_f32_workspace": (i64, [i32] * 9),
         "eosv_flip_weights": (i32, [vp, i32, i32, i32, i32, vp, vp]),
         "eosv_sgemm_tn_splitk_workspace": (i64, [i32, i32, i32]),
         "eosv_sgemm_tn_splitk": (i32, [i32, i32, i32, vp, i32, vp, i32, vp, i32, vp, i64, vp]),

@@ -180,8 +180,10 @@ class NativeTrainer:
         P = N * Ho * Wo
         y = torch.empty(P * c.cout, dtype=torch.float32, device=self.dev)
         # the inference conv kernels (exact-f32 MFMA) where they apply, else im2col + rocBLAS
+        kb = int(self.L.eosv_conv2d_f32_workspace(N, H, W, c.cin, c.cout, c.k, c.k, c.stride, c.pad))
+        kw = self._buf("ksplit", kb // 4 + 4)
         rc = self.L.eosv_conv2d_f32(_f(x), N, H, W, c.cin, _f(c.w), c.cout, c.k, c.k, c.stride, c.pad, None, None, 0,
-                                    _f(y), s)
+                                    _f(y), _f(kw), kb, s)
         if rc == _UNSUPPORTED:
             if c.k == 1 and c.stride == 1:
                 col = x
@@ -227,8 +229,10 @@ class NativeTrainer:
             # stride 1: dx = conv(dz, W flipped and transposed) on the inference conv kernels
             wf = self._buf("wflip", c.cout * c.K)
             check(self.L.eosv_flip_weights(_f(c.w), c.cout, c.k, c.k, c.cin, _f(wf), s), "eosv_flip_weights")
+            kb = int(self.L.eosv_conv2d_f32_workspace(N, Ho, Wo, c.cout, c.cin, c.k, c.k, 1, c.pad))
+            kw = self._buf("ksplit", kb // 4 + 4)
             rc = self.L.eosv_conv2d_f32(_f(dz), N, Ho, Wo, c.cout, _f(wf), c.cin, c.k, c.k, 1, c.pad, None, _f(acc),
-                                        0, _f(dx), s)
+                                        0, _f(dx), _f(kw), kb, s)
             if rc != _UNSUPPORTED:
                 check(rc, "eosv_conv2d_f32")
                 return dx

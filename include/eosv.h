@@ -248,8 +248,13 @@ int eosv_sgd_momentum(float* d_p, const float* d_g, float* d_buf, int64_t n, flo
  * forward of every conv but the stem, and, with eosv_flip_weights' [Cin][KH][KW][Cout] weights,
  * the input gradient of the stride-1 convs.  EOSV_ERR_UNSUPPORTED unless Cin % 32 == 0. */
 int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_w, int Cout, int KH, int KW,
-                    int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y,
-                    eosv_stream_t stream);
+                    int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y, float* d_work,
+                    int64_t work_bytes, eosv_stream_t stream);
+/* Optional workspace of eosv_conv2d_f32 (d_work / work_bytes; NULL / 0 = none): with it, a launch
+ * whose grid would leave CUs idle splits its K loop over up to 8 slices of raw partial sums,
+ * summed in slice order with the bias / residual / ReLU epilogue (deterministic, not bitwise
+ * equal to the unsplit order). */
+int64_t eosv_conv2d_f32_workspace(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int eosv_flip_weights(const float* d_w, int Cout, int KH, int KW, int Cin, float* d_wf, eosv_stream_t stream);
 /* y += alpha x; NCHW -> NHWC. */
 int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_t stream);

@@ -184,8 +184,15 @@ def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
 
     yd = torch.empty(P * cout, device="cuda")
     _call(L.eosv_conv2d_f32, xd.data_ptr(), N, H, H, cin, wd.data_ptr(), cout, k, k, stride, pad, None, None, 0,
-          yd.data_ptr())
+          yd.data_ptr(), None, 0)
     assert rel(yd.view(N, Ho, Wo, cout).permute(0, 3, 1, 2), y.detach()) < 1e-5
+    # with a workspace: split-K over slices (small grids), same result within f32 rounding
+    kb = int(L.eosv_conv2d_f32_workspace(N, H, H, cin, cout, k, k, stride, pad))
+    kws = torch.empty(kb // 4 + 4, device="cuda")
+    yk = torch.full_like(yd, float("nan"))
+    _call(L.eosv_conv2d_f32, xd.data_ptr(), N, H, H, cin, wd.data_ptr(), cout, k, k, stride, pad, None, None, 0,
+          yk.data_ptr(), kws.data_ptr(), kb)
+    assert rel(yk.view(N, Ho, Wo, cout).permute(0, 3, 1, 2), y.detach()) < 1e-5
     col = torch.empty(P * K, device="cuda")
     _call(L.eosv_im2col, xd.data_ptr(), N, H, H, cin, k, k, stride, pad, col.data_ptr())
     wb = int(L.eosv_sgemm_tn_splitk_workspace(cout, K, P))
@@ -207,14 +214,17 @@ def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
         _call(L.eosv_flip_weights, wd.data_ptr(), cout, k, k, cin, wf.data_ptr())
         gx = torch.empty(N * H * H * cin, device="cuda")
         _call(L.eosv_conv2d_f32, dyd.data_ptr(), N, Ho, Wo, cout, wf.data_ptr(), cin, k, k, 1, pad, None, None, 0,
-              gx.data_ptr())
+              gx.data_ptr(), None, 0)
         assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad) < 1e-5
         # the shortcut's gradient fused as the epilogue residual (the trainer's first-conv dgrad)
         sk = torch.randn(N, H, H, cin, dtype=torch.float64)
         skd = sk.float().cuda().contiguous()
-        _call(L.eosv_conv2d_f32, dyd.data_ptr(), N, Ho, Wo, cout, wf.data_ptr(), cin, k, k, 1, pad, None,
-              skd.data_ptr(), 0, gx.data_ptr())
-        assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad + sk.permute(0, 3, 1, 2)) < 1e-5
+        kb = int(L.eosv_conv2d_f32_workspace(N, Ho, Wo, cout, cin, k, k, 1, pad))
+        kws = torch.empty(kb // 4 + 4, device="cuda")
+        for ws, wsb in ((None, 0), (kws.data_ptr(), kb)):
+            _call(L.eosv_conv2d_f32, dyd.data_ptr(), N, Ho, Wo, cout, wf.data_ptr(), cin, k, k, 1, pad, None,
+                  skd.data_ptr(), 0, gx.data_ptr(), ws, wsb)
+            assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad + sk.permute(0, 3, 1, 2)) < 1e-5
 
 
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
