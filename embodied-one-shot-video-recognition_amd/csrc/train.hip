@@ -383,6 +383,70 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int* __re
   }
 }
 
+// the same two passes over 4 channels per thread (C % 4 == 0, 16-byte aligned): one pixel's
+// window / pooled neighbours as float4 and int4 accesses, 32-bit pixel indexing
+__global__ void maxpool_fwd4_kernel(const float4* __restrict__ x, int NP, int H, int W, int C4, int Ho, int Wo,
+                                    float4* __restrict__ y, int4* __restrict__ idx) {
+  const long long total = (long long)NP * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    const int r = (int)(i / C4);
+    const int ow = r % Wo, r2 = r / Wo;
+    const int oh = r2 % Ho, n = r2 / Ho;
+    float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int arg[4] = {-1, -1, -1, -1};
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const float4 v = x[((long long)(n * H + ih) * W + iw) * C4 + c4];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4; ++j)
+          if (vv[j] > m[j] || arg[j] < 0) m[j] = vv[j], arg[j] = ih * W + iw;
+      }
+    }
+    y[i] = make_float4(m[0], m[1], m[2], m[3]);
+    idx[i] = make_int4(arg[0], arg[1], arg[2], arg[3]);
+  }
+}
+
+__global__ void maxpool_bwd4_kernel(const float4* __restrict__ dy, const int4* __restrict__ idx, int NP, int H, int W,
+                                    int C4, int Ho, int Wo, float4* __restrict__ dx) {
+  const long long total = (long long)NP * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    const int r = (int)(i / C4);
+    const int iw = r % W, r2 = r / W;
+    const int ih = r2 % H, n = r2 / H;
+    const int me = ih * W + iw;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int kh = 0; kh < 3; ++kh) {
+      const int th = ih + 1 - kh;
+      if (th < 0 || (th & 1)) continue;
+      const int oh = th >> 1;
+      if (oh >= Ho) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tw = iw + 1 - kw;
+        if (tw < 0 || (tw & 1)) continue;
+        const int ow = tw >> 1;
+        if (ow >= Wo) continue;
+        const long long o = ((long long)(n * Ho + oh) * Wo + ow) * C4 + c4;
+        const int4 a = idx[o];
+        const float4 d = dy[o];
+        if (a.x == me) s[0] += d.x;
+        if (a.y == me) s[1] += d.y;
+        if (a.z == me) s[2] += d.z;
+        if (a.w == me) s[3] += d.w;
+      }
+    }
+    dx[i] = make_float4(s[0], s[1], s[2], s[3]);
+  }
+}
+
 // y[n][c] = mean over HW of x[n][hw][c] (sequential); backward dx = dy / HW
 __global__ void avgpool_fwd_kernel(const float* __restrict__ x, int N, int HW, int C, float* __restrict__ y) {
   const long long total = (long long)N * C;
@@ -709,8 +773,13 @@ int eosv_maxpool_forward(const float* d_x, int N, int H, int W, int C, float* d_
   if (!d_x || !d_y || !d_idx || N <= 0 || H <= 0 || W <= 0 || C <= 0)
     return set_error("eosv_maxpool_forward: bad argument"), EOSV_ERR_ARG;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0,
-                     (hipStream_t)stream, d_x, N, H, W, C, Ho, Wo, d_y, d_idx);
+  if (C % 4 == 0 && al16(d_x) && al16(d_y) && al16(d_idx) && (long long)N * H * W < (1LL << 31))
+    hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3(grid_for((long long)N * Ho * Wo * C / 4)), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)d_x, N * Ho * Wo, H, W, C / 4, Ho, Wo, (float4*)d_y,
+                       (int4*)d_idx);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * Ho * Wo * C)), dim3(256), 0,
+                       (hipStream_t)stream, d_x, N, H, W, C, Ho, Wo, d_y, d_idx);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -720,8 +789,13 @@ int eosv_maxpool_backward(const float* d_dy, const int32_t* d_idx, int N, int H,
   if (!d_dy || !d_idx || !d_dx || N <= 0 || H <= 0 || W <= 0 || C <= 0)
     return set_error("eosv_maxpool_backward: bad argument"), EOSV_ERR_ARG;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
-                     d_dy, d_idx, N, H, W, C, Ho, Wo, d_dx);
+  if (C % 4 == 0 && al16(d_dy) && al16(d_idx) && al16(d_dx) && (long long)N * H * W < (1LL << 31))
+    hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3(grid_for((long long)N * H * W * C / 4)), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)d_dy, (const int4*)d_idx, N * H * W, H, W, C / 4, Ho, Wo,
+                       (float4*)d_dx);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
+                       d_dy, d_idx, N, H, W, C, Ho, Wo, d_dx);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

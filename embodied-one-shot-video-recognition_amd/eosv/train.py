@@ -134,18 +134,33 @@ class NativeTrainer:
             v = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
             return v.detach().to(self.dev, torch.float32).contiguous()
 
+        # optimizer_1's parameters (convnet: conv weights, BN gamma / beta) live in one flat buffer
+        # (each tensor 16-byte aligned), with flat gradient and momentum buffers: one SGD launch
+        sizes = [c.cout * c.K for c in self._convs()] + [b.c for b in self._bns() for _ in range(2)]
+        total = sum((n + 3) // 4 * 4 for n in sizes)
+        self.p_flat = torch.zeros(total, dtype=torch.float32, device=self.dev)
+        self.g_flat = torch.zeros_like(self.p_flat)
+        self.m_flat = torch.zeros_like(self.p_flat)
+        off = [0]
+
+        def views(n):
+            o = off[0]
+            off[0] += (n + 3) // 4 * 4
+            return self.p_flat[o:o + n], self.g_flat[o:o + n], self.m_flat[o:o + n]
+
         for c in self._convs():
             w = t(c.name + ".weight")                       # [Cout][Cin][KH][KW]
-            c.w = w.permute(0, 2, 3, 1).reshape(c.cout, c.K).contiguous()
-            c.g = torch.zeros_like(c.w)
-            c.buf = torch.zeros_like(c.w)
+            p, g, m = views(c.cout * c.K)
+            p.copy_(w.permute(0, 2, 3, 1).reshape(-1))
+            c.w, c.g, c.buf = p.view(c.cout, c.K), g.view(c.cout, c.K), m.view(c.cout, c.K)
         for b in self._bns():
-            b.gamma, b.beta = t(b.name + ".weight"), t(b.name + ".bias")
+            b.gamma, b.dgamma, b.buf_g = views(b.c)
+            b.beta, b.dbeta, b.buf_b = views(b.c)
+            b.gamma.copy_(t(b.name + ".weight"))
+            b.beta.copy_(t(b.name + ".bias"))
             b.rm, b.rv = t(b.name + ".running_mean"), t(b.name + ".running_var")
             nbt = sd.get(b.name + ".num_batches_tracked", 0)
             b.nbt = int(nbt.item() if isinstance(nbt, torch.Tensor) else np.asarray(nbt))
-            b.dgamma, b.dbeta = torch.zeros_like(b.gamma), torch.zeros_like(b.beta)
-            b.buf_g, b.buf_b = torch.zeros_like(b.gamma), torch.zeros_like(b.beta)
         self.fc_w, self.fc_b = t("fc.weight"), t("fc.bias")
         self.fc_gw, self.fc_gb = torch.zeros_like(self.fc_w), torch.zeros_like(self.fc_b)
         self.fc_bw, self.fc_bb = torch.zeros_like(self.fc_w), torch.zeros_like(self.fc_b)
@@ -365,11 +380,8 @@ class NativeTrainer:
         self._conv_bwd(dz0, x0, shp0, self.stem, s, need_dx=False)
         # ---- SGD (optimizer_1: convnet, optimizer_2: fc; first step initialises the momentum)
         first = int(self.step_count == 0)
-        for c in self._convs():
-            check(L.eosv_sgd_momentum(_f(c.w), _f(c.g), _f(c.buf), c.w.numel(), lr_conv, momentum, first, s), "sgd")
-        for b in self._bns():
-            check(L.eosv_sgd_momentum(_f(b.gamma), _f(b.dgamma), _f(b.buf_g), b.c, lr_conv, momentum, first, s), "sgd")
-            check(L.eosv_sgd_momentum(_f(b.beta), _f(b.dbeta), _f(b.buf_b), b.c, lr_conv, momentum, first, s), "sgd")
+        check(L.eosv_sgd_momentum(_f(self.p_flat), _f(self.g_flat), _f(self.m_flat), self.p_flat.numel(), lr_conv,
+                                  momentum, first, s), "sgd")
         check(L.eosv_sgd_momentum(_f(self.fc_w), _f(self.fc_gw), _f(self.fc_bw), self.fc_w.numel(), lr_fc, momentum,
                                   first, s), "sgd")
         check(L.eosv_sgd_momentum(_f(self.fc_b), _f(self.fc_gb), _f(self.fc_bb), self.fc_b.numel(), lr_fc, momentum,

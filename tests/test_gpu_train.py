@@ -278,12 +278,13 @@ def test_batchnorm_train_forward_backward_vs_torch(relu, res):
         assert rel(back(dres), r.grad) < 1e-6
 
 
-def test_maxpool_forward_backward_vs_torch():
+@pytest.mark.parametrize("C", [5, 12])  # scalar and float4 kernels
+def test_maxpool_forward_backward_vs_torch(C):
     from eosv._lib import lib
 
     L = lib()
     torch.manual_seed(3)
-    N, C, H, W = 2, 5, 9, 8
+    N, H, W = 2, 9, 8
     x = torch.randn(N, C, H, W, dtype=torch.float64, requires_grad=True)
     y = torch.nn.functional.max_pool2d(x, 3, 2, 1)
     dy = torch.randn_like(y)
@@ -297,6 +298,9 @@ def test_maxpool_forward_backward_vs_torch():
     dx = torch.empty(N * H * W * C, device="cuda")
     _call(L.eosv_maxpool_backward, dyd.data_ptr(), idx.data_ptr(), N, H, W, C, dx.data_ptr())
     assert torch.equal(yd.view(N, Ho, Wo, C).permute(0, 3, 1, 2).cpu(), y.detach().float())
+    # the argmax is torch CPU's (first maximum in window order)
+    ref_idx = torch.nn.functional.max_pool2d(x.detach(), 3, 2, 1, return_indices=True)[1]
+    assert torch.equal(idx.view(N, Ho, Wo, C).permute(0, 3, 1, 2).cpu().long(), ref_idx)
     assert torch.allclose(dx.view(N, H, W, C).permute(0, 3, 1, 2).double().cpu(), x.grad, rtol=0, atol=1e-6)
 
 
