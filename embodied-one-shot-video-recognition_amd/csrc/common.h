@@ -89,12 +89,15 @@ struct ConvArgs {
   // (0 = derive; conv_pixel_strides)
   int xs, x2s;
   LaunchInfo* plan;   // host-side: non-null = record the grid (record_launch), launch nothing
-  // f32 implicit GEMM only (the training entry eosv_conv2d_f32): split the K loop over
-  // gridDim.y = ksplit slices writing raw partial sums to kws ([ksplit][M][Cout]); the launcher
-  // then sums them in slice order with the bias / residual / ReLU epilogue.  0 / 1 = off.
-  int ksplit;
+  // f32 implicit GEMM only (the training entry eosv_conv2d_f32): with a workspace, a small grid
+  // splits the K loop over gridDim.y slices writing raw partial sums to kws ([slices][M][Cout],
+  // kws_bytes large enough, else no split); the launcher then sums them in slice order with the
+  // bias / residual / ReLU epilogue.
   float* kws;
+  long long kws_bytes;
 };
+// the K-slice count launch_conv_f32 would use for `a` given a large enough workspace (1 = none)
+int conv_f32_ksplit_slices(const ConvArgs& a);
 
 __host__ __device__ inline int split_chan(int c, int cin3) {
   const int c2 = 2 * (cin3 / 3);

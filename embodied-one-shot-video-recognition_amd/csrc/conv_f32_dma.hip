@@ -302,6 +302,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   }
 }
 
+// split-K (training entry only): enough slices to put ~2 workgroups on every CU, each slice at
+// least 32 K-steps, at most 8
+static int ksplit_count(long long blocks, int ksteps) {
+  const long long want = (2LL * device_cu_count() + blocks - 1) / blocks;
+  return (int)std::max(1LL, std::min({want, (long long)ksteps / 32, 8LL}));
+}
+
 // split-K epilogue: y = relu(sum over slices (in order) + bias + residual), float4 over Cout
 __global__ void ksplit_sum_kernel(const float4* __restrict__ ws, int ks, long long mc4, int C4,
                                   const float* __restrict__ bias, const float4* __restrict__ res, int relu,
@@ -344,12 +351,10 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
         (const void*)conv_f32_dma_kernel<BM, BN, BK, WM, WN, false, NS, EPI, false>, 64 * WM * WN);
     return record_launch(a.plan, nb, occ);
   }
-  // split-K (training entry only): enough slices to put ~2 workgroups on every CU, each slice
-  // at least 32 K-steps
   int ks = 1;
   if (a.kws && !STEM && !a.x2 && EPI) {
-    const long long want = (2LL * device_cu_count() + nb - 1) / nb;
-    ks = (int)std::max(1LL, std::min({want, (long long)(a.K / BK) / 32, 8LL}));
+    ks = ksplit_count(nb, a.K / BK);
+    if ((long long)ks * M * a.Cout * (long long)sizeof(float) > a.kws_bytes) ks = 1;
   }
   if (a.x2) {
     if (STEM || a.K1 % BK || a.Cin2 % BK) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
@@ -362,6 +367,17 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
   EOSV_LAUNCH_CHECK();
   if (ks > 1) return launch_ksplit_sum(a, ks, M, s);
   return EOSV_OK;
+}
+
+// Cout > 64 tiles: small batches (the training step: 96 frames) give grids below the chip's CU
+// count, so the tile shrinks (same BK, same k-order per output: bit-identical results).
+// 1 = 256x128, 2 = 128x128, 3 = 128x64.
+static int f32_tile(const ConvArgs& a) {
+  const long long M = (long long)a.N * a.Ho * a.Wo, cus = device_cu_count();
+  auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
+  if (a.Cout <= 256 && blocks(256, 128) >= cus) return 1;
+  if (blocks(128, 128) >= cus) return 2;
+  return 3;
 }
 
 // Tile per layer (r01 / r01l A/B): 256x64 (4 waves of 64x64) for Cout 64, 256x128
@@ -397,13 +413,20 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
   if (tile == 5) return launch_dma<512, 128, 16, 4, 2, false>(a, s);  // 8 waves of 128x64
   if (tile == 6 && a.Cout <= 256) return launch_dma<512, 128, 16, 4, 2, false>(a, s);
 #endif
-  // small batches (the training step: 96 frames): a grid below the chip's CU count leaves
-  // CUs idle, so the tile shrinks (same BK, same k-order per output: bit-identical results)
-  const long long M = (long long)a.N * a.Ho * a.Wo, cus = device_cu_count();
-  auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
-  if (a.Cout <= 256 && blocks(256, 128) >= cus) return launch_dma<256, 128, 16, 4, 2, false>(a, s);
-  if (blocks(128, 128) >= cus) return launch_dma<128, 128, 16, 2, 2, false>(a, s);
-  return launch_dma<128, 64, 16, 2, 2, false>(a, s);
+  switch (f32_tile(a)) {
+    case 1: return launch_dma<256, 128, 16, 4, 2, false>(a, s);
+    case 2: return launch_dma<128, 128, 16, 2, 2, false>(a, s);
+    default: return launch_dma<128, 64, 16, 2, 2, false>(a, s);
+  }
+}
+
+int conv_f32_ksplit_slices(const ConvArgs& a) {
+  if (a.Cin == 3 || a.x2 || a.Cout % 4 || a.Cout <= 64 || a.K % 32 || a.Cin % 32) return 1;
+  if (env_switch("EOSV_F32_ROWS", 1) && conv_rows_f32_ok(a)) return 1;
+  static const int bm[] = {0, 256, 128, 128}, bn[] = {0, 128, 128, 64};
+  const int t = f32_tile(a);
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  return ksplit_count(((M + bm[t] - 1) / bm[t]) * ((a.Cout + bn[t] - 1) / bn[t]), a.K / 16);
 }
 
 }  // namespace eosv

@@ -858,11 +858,22 @@ int eosv_axpy(float* d_y, const float* d_x, int64_t n, float alpha, eosv_stream_
   return EOSV_OK;
 }
 
+static ConvArgs conv2d_args(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad) {
+  ConvArgs a{};
+  a.N = N, a.H = H, a.W = W, a.Cin = Cin;
+  a.Ho = (H + 2 * pad - KH) / stride + 1, a.Wo = (W + 2 * pad - KW) / stride + 1, a.Cout = Cout;
+  a.KH = KH, a.KW = KW, a.KWp = KW, a.stride = stride, a.pad = pad;
+  a.K = KH * KW * Cin;
+  a.xcd = 1;
+  return a;
+}
+
 int64_t eosv_conv2d_f32_workspace(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad) {
   if (N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0) return 0;
-  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
-  if (Ho <= 0 || Wo <= 0) return 0;
-  return (int64_t)8 * N * Ho * Wo * Cout * (int64_t)sizeof(float);  // up to 8 K-slices
+  const ConvArgs a = conv2d_args(N, H, W, Cin, Cout, KH, KW, stride, pad);
+  if (a.Ho <= 0 || a.Wo <= 0) return 0;
+  const int ks = conv_f32_ksplit_slices(a);  // the slices the launch will use (1: no workspace)
+  return ks > 1 ? (int64_t)ks * N * a.Ho * a.Wo * Cout * (int64_t)sizeof(float) : 0;
 }
 
 int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_w, int Cout, int KH, int KW,
@@ -878,23 +889,16 @@ int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float*
            EOSV_ERR_UNSUPPORTED;
   int dev = 0;
   EOSV_HIP_CHECK(hipGetDevice(&dev));
-  ConvArgs a{};
+  ConvArgs a = conv2d_args(N, H, W, Cin, Cout, KH, KW, stride, pad);
   a.x = d_x;
   a.w = d_w;
   a.bias = d_bias;
   a.res = d_res;
   a.y = d_y;
-  a.N = N, a.H = H, a.W = W, a.Cin = Cin;
-  a.Ho = Ho, a.Wo = Wo, a.Cout = Cout;
-  a.KH = KH, a.KW = KW, a.KWp = KW, a.stride = stride, a.pad = pad;
-  a.K = KH * KW * Cin;
   a.relu = relu;
   a.zero = zero_page(dev);
-  a.xcd = 1;
   // split-K over the workspace when one is given (small grids: the training batch)
-  if (d_work && work_bytes >= eosv_conv2d_f32_workspace(N, H, W, Cin, Cout, KH, KW, stride, pad) &&
-      !((uintptr_t)d_work & 15))
-    a.kws = d_work;
+  if (d_work && work_bytes > 0 && !((uintptr_t)d_work & 15)) a.kws = d_work, a.kws_bytes = work_bytes;
   if (!a.zero) return set_error("eosv_conv2d_f32: zero page allocation failed"), EOSV_ERR_OOM;
   return launch_conv_f32(a, (hipStream_t)stream);
 }

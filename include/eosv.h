@@ -250,7 +250,7 @@ int eosv_sgd_momentum(float* d_p, const float* d_g, float* d_buf, int64_t n, flo
 int eosv_conv2d_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_w, int Cout, int KH, int KW,
                     int stride, int pad, const float* d_bias, const float* d_res, int relu, float* d_y, float* d_work,
                     int64_t work_bytes, eosv_stream_t stream);
-/* Optional workspace of eosv_conv2d_f32 (d_work / work_bytes; NULL / 0 = none): with it, a launch
+/* Workspace of eosv_conv2d_f32 (d_work / work_bytes; NULL / 0 = none; 0 bytes needed = no split): a launch
  * whose grid would leave CUs idle splits its K loop over up to 8 slices of raw partial sums,
  * summed in slice order with the bias / residual / ReLU epilogue (deterministic, not bitwise
  * equal to the unsplit order). */
