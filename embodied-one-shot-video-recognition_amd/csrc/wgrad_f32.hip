@@ -169,15 +169,18 @@ struct WgradPlan {
   long long slices, rows;
 };
 
-// tile: 64 x 192 (1 x 3 waves) for Cout 64, 128 x 128 (2 x 2) for Cout % 128 == 0; slices so that
-// tiles x slices is ~4 blocks per CU, at least 256 pixel rows each
+// tile: the first of 128 x 128 (2 x 2 waves), 64 x 256, 64 x 192, 128 x 64, 64 x 128, 64 x 64 that
+// divides (Cout, K); slices so that tiles x slices is ~4 blocks per CU, at least 256 pixel rows each
 bool wgrad_plan(int Cout, int K, long long P, WgradPlan* pl) {
-  if (Cout % 128 == 0 && K % 128 == 0)
-    pl->wm = 2, pl->wn = 2;
-  else if (Cout % 64 == 0 && K % 192 == 0)
-    pl->wm = 1, pl->wn = 3;
-  else
-    return false;
+  static const int cand[][2] = {{2, 2}, {1, 4}, {1, 3}, {2, 1}, {1, 2}, {1, 1}};
+  bool ok = false;
+  for (const auto& c : cand)
+    if (Cout % (64 * c[0]) == 0 && K % (64 * c[1]) == 0) {
+      pl->wm = c[0], pl->wn = c[1];
+      ok = true;
+      break;
+    }
+  if (!ok) return false;
   pl->co_tiles = Cout / (64 * pl->wm);
   pl->k_tiles = K / (64 * pl->wn);
   const long long tiles = (long long)pl->co_tiles * pl->k_tiles;
@@ -225,8 +228,8 @@ int eosv_conv_wgrad_f32(const float* d_x, int N, int H, int W, int Cin, const fl
   const int K = KH * KW * Cin;
   WgradPlan pl;
   if (Cin % 4 || ((uintptr_t)d_x | (uintptr_t)d_dy | (uintptr_t)d_dw) & 15 || !wgrad_plan(Cout, K, (long long)N * Ho * Wo, &pl))
-    return set_error("eosv_conv_wgrad_f32: needs Cin % 4 == 0, 16-byte aligned operands and Cout % 128 / K % 128 "
-                     "or Cout % 64 / K % 192"),
+    return set_error("eosv_conv_wgrad_f32: needs Cin % 4 == 0, 16-byte aligned operands, Cout % 64 == 0 and "
+                     "K % 64 == 0"),
            EOSV_ERR_UNSUPPORTED;
   const int64_t need = eosv_conv_wgrad_f32_workspace(N, H, W, Cin, Cout, KH, KW, stride, pad);
   if (need > 0 && (!d_work || work_bytes < need || ((uintptr_t)d_work & 15)))
@@ -239,10 +242,15 @@ int eosv_conv_wgrad_f32(const float* d_x, int N, int H, int W, int Cin, const fl
   const long long blocks = pl.slices * pl.co_tiles * pl.k_tiles;
   if (blocks > 0x7fffffffLL) return set_error("eosv_conv_wgrad_f32: grid too large"), EOSV_ERR_UNSUPPORTED;
   const hipStream_t s = (hipStream_t)stream;
-  if (pl.wm == 2)
-    hipLaunchKernelGGL((wgrad_f32_kernel<2, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((wgrad_f32_kernel<1, 3>), dim3((unsigned)blocks), dim3(192), 0, s, a);
+  const dim3 g((unsigned)blocks), b(64 * pl.wm * pl.wn);
+  switch (pl.wm * 10 + pl.wn) {
+    case 22: hipLaunchKernelGGL((wgrad_f32_kernel<2, 2>), g, b, 0, s, a); break;
+    case 14: hipLaunchKernelGGL((wgrad_f32_kernel<1, 4>), g, b, 0, s, a); break;
+    case 13: hipLaunchKernelGGL((wgrad_f32_kernel<1, 3>), g, b, 0, s, a); break;
+    case 21: hipLaunchKernelGGL((wgrad_f32_kernel<2, 1>), g, b, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((wgrad_f32_kernel<1, 2>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((wgrad_f32_kernel<1, 1>), g, b, 0, s, a); break;
+  }
   EOSV_LAUNCH_CHECK();
   if (pl.slices > 1) {
     const long long mn = (long long)Cout * K;

@@ -219,8 +219,10 @@ class NativeTrainer:
         P = N * Ho * Wo
         direct = c.k == 1 and c.stride == 1
         rc = _UNSUPPORTED
-        if c.k > 1:
-            # KxK: implicit-GEMM weight gradient (no im2col buffer)
+        if c.cin % 4 == 0 and not direct:
+            # KxK and strided 1x1: implicit-GEMM weight gradient (no im2col buffer).  Stride-1 1x1
+            # convs stay on rocBLAS (X is already the GEMM operand; measured faster on 9 of the 11
+            # R50 shapes, tools/bench_train_convs.py)
             wb = int(self.L.eosv_conv_wgrad_f32_workspace(N, H, W, c.cin, c.cout, c.k, c.k, c.stride, c.pad))
             ws = self._buf("splitk", wb // 4 + 4)
             rc = self.L.eosv_conv_wgrad_f32(_f(x), N, H, W, c.cin, _f(dz), c.cout, c.k, c.k, c.stride, c.pad, _f(c.g),

@@ -200,8 +200,8 @@ int eosv_sgemm_tn_splitk(int m, int n, int k, const float* d_a, int lda, const f
 /* Weight gradient of a KxK conv without the im2col buffer: dW[Cout][KH][KW][Cin] = sum over
  * output pixels of dY[p][co] * X[in(p, kh, kw)][ci] (NHWC x [N][H][W][Cin], dY [P][Cout]), an
  * implicit GEMM on exact-f32 MFMA with the pixel reduction split into slices summed in order
- * (deterministic).  EOSV_ERR_UNSUPPORTED unless Cin % 4 == 0 and (Cout % 128, K % 128) or
- * (Cout % 64, K % 192), K = KH KW Cin; d_work: eosv_conv_wgrad_f32_workspace(...) bytes. */
+ * (deterministic).  EOSV_ERR_UNSUPPORTED unless Cin % 4 == 0, Cout % 64 == 0 and K % 64 == 0,
+ * K = KH KW Cin; d_work: eosv_conv_wgrad_f32_workspace(...) bytes. */
 int64_t eosv_conv_wgrad_f32_workspace(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int eosv_conv_wgrad_f32(const float* d_x, int N, int H, int W, int Cin, const float* d_dy, int Cout, int KH, int KW,
                         int stride, int pad, float* d_dw, float* d_work, int64_t work_bytes, eosv_stream_t stream);

@@ -156,7 +156,8 @@ def test_conv_forward_and_gradients_vs_torch(k, stride, pad, cin, cout):
 
 @pytest.mark.parametrize("k,stride,cin,cout,H", [(3, 1, 64, 64, 56), (3, 1, 128, 64, 14), (1, 1, 64, 256, 28),
                                                  (3, 2, 64, 128, 28), (1, 2, 256, 512, 14), (3, 1, 128, 256, 13),
-                                                 (3, 2, 256, 512, 15)])
+                                                 (3, 2, 256, 512, 15), (1, 1, 256, 64, 28), (1, 1, 64, 128, 14),
+                                                 (1, 1, 128, 64, 14)])
 def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
     """The trainer's fast paths: eosv_conv2d_f32 forward (the inference conv kernels, exact f32),
     the stride-1 input gradient as a conv of dY with eosv_flip_weights' weights, the split-K
@@ -201,14 +202,13 @@ def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
     _call(L.eosv_sgemm_tn_splitk, cout, K, P, dyd.data_ptr(), cout, col.data_ptr(), K, gw.data_ptr(), K,
           ws.data_ptr(), wb)
     assert rel(gw.view(cout, k, k, cin).permute(0, 3, 1, 2), w.grad) < 1e-5
-    if k > 1:
-        # the implicit-GEMM weight gradient (no im2col buffer)
-        wb = int(L.eosv_conv_wgrad_f32_workspace(N, H, H, cin, cout, k, k, stride, pad))
-        ws = torch.empty(wb // 4 + 4, device="cuda")
-        gw2 = torch.full((cout * K,), float("nan"), device="cuda")
-        _call(L.eosv_conv_wgrad_f32, xd.data_ptr(), N, H, H, cin, dyd.data_ptr(), cout, k, k, stride, pad,
-              gw2.data_ptr(), ws.data_ptr(), wb)
-        assert rel(gw2.view(cout, k, k, cin).permute(0, 3, 1, 2), w.grad) < 1e-5
+    # the implicit-GEMM weight gradient (no im2col buffer; every tile shape across the cases)
+    wb = int(L.eosv_conv_wgrad_f32_workspace(N, H, H, cin, cout, k, k, stride, pad))
+    ws = torch.empty(wb // 4 + 4, device="cuda")
+    gw2 = torch.full((cout * K,), float("nan"), device="cuda")
+    _call(L.eosv_conv_wgrad_f32, xd.data_ptr(), N, H, H, cin, dyd.data_ptr(), cout, k, k, stride, pad,
+          gw2.data_ptr(), ws.data_ptr(), wb)
+    assert rel(gw2.view(cout, k, k, cin).permute(0, 3, 1, 2), w.grad) < 1e-5
     if stride == 1:
         wf = torch.empty(cout * K, device="cuda")
         _call(L.eosv_flip_weights, wd.data_ptr(), cout, k, k, cin, wf.data_ptr())

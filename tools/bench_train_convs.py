@@ -26,7 +26,7 @@ for li, (planes, nb) in enumerate(zip((64, 128, 256, 512), (3, 4, 6, 3))):
         H, inpl = Ho, planes * 4
 seen = set()
 s = stream_ptr()
-tot = {"fwd": [0, 0], "fwdk": [0, 0], "wgrad": [0, 0]}
+tot = {"fwd": [0, 0], "fwdk": [0, 0], "wgrad": [0, 0], "wgrad_blas": [0, 0]}
 for name, H, cin, cout, k, st in shapes:
     key = (H, cin, cout, k, st)
     if key in seen:
@@ -57,8 +57,18 @@ for name, H, cin, cout, k, st in shapes:
         return lambda: check(L.eosv_conv_wgrad_f32(x.data_ptr(), N, H, H, cin, y.data_ptr(), cout, k, k, st, pad,
                                                    g.data_ptr(), ws.data_ptr(), wb, s), "wgrad")
 
+    def wgb():
+        if k != 1 or st != 1:
+            return None
+        P = N * Ho * Ho
+        wb = int(L.eosv_sgemm_tn_splitk_workspace(cout, cin, P))
+        ws = torch.empty(wb // 4 + 4, device="cuda")
+        g = torch.empty(cout * cin, device="cuda")
+        return lambda: check(L.eosv_sgemm_tn_splitk(cout, cin, P, y.data_ptr(), cout, x.data_ptr(), cin, g.data_ptr(),
+                                                    cin, ws.data_ptr(), wb, s), "wgrad_blas")
+
     out = [name, f"{H}x{H} {cin}->{cout} k{k} s{st}"]
-    for tag, fn in (("fwd", fwd), ("fwdk", fwdk), ("wgrad", wg() if k > 1 else None)):
+    for tag, fn in (("fwd", fwd), ("fwdk", fwdk), ("wgrad", wg()), ("wgrad_blas", wgb())):
         if fn is None:
             continue
         for _ in range(3):
