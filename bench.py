@@ -32,7 +32,8 @@ MFMA_PEAK_TF = {"f32": 157.3, "bf16": 2516.6}  # MI355X dense peaks (MI355X_MICR
 # f32x3 (EOSV_F32X3): every f32-accurate product is three bf16 MFMA products, so its ceiling in
 # algorithmic (f32) FLOP/s is the bf16 dense peak / 3
 MFMA_PEAK_TF["f32x3"] = round(MFMA_PEAK_TF["bf16"] / 3, 1)
-ELEM_BYTES = {"f32": 4, "bf16": 2, "f32x3": 6}  # activation bytes per element (f32x3: hi, lo, hi)
+ELEM_BYTES = {"f32": 4, "bf16": 2, "f32x3": 4}  # stored activation bytes per element (f32x3: the (hi, lo) pair)
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -174,15 +175,60 @@ def measured_traffic(dtype, key):
 
 
 def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches, chunks):
-    """Conv-family algorithmic bytes per launch: every layer's input + output (+ residual) map
-    once per frame and its weights once per chunk (arch.conv_layer_bytes: the unfused plan's
-    floor; with the downsample folded into the block's last conv there are fewer launches)."""
-    elem = ELEM_BYTES[dtype]
-    layers = arch_mod.conv_layer_bytes(arch_mod.SPECS[args.arch], args.res, args.res, elem,
-                                       stem_pool_fused=(dtype != "f32"))
-    per_frame = sum(b for b, _ in layers)
-    weights = sum(w for _, w in layers)
+    """Conv-family algorithmic bytes per launch: every launch's input + output (+ residual or
+    folded-downsample input) map once per frame and its weights once per chunk
+    (arch.conv_launch_bytes: the fused stem + pool reads the f32 frame and writes the pooled map)."""
+    layers = arch_mod.conv_launch_bytes(arch_mod.SPECS[args.arch], args.res, args.res, ELEM_BYTES[dtype])
+    per_frame = sum(e[0] for e in layers)
+    weights = sum(e[1] for e in layers)
     return (frames * per_frame + chunks * weights) / launches
+
+
+def layer_bounds(prof, dtype, args, arch_mod, frames):
+    """Per-launch roofline of the timed region: for every conv layer, its floor time is
+    max(algorithmic FLOPs / MFMA peak, algorithmic bytes (arch.conv_launch_bytes) / HBM peak);
+    frac = sum of floors / sum of measured HIP-event times.  A layer is 'hbm'-bound when the byte
+    floor is the larger (R50's 1x1 convs at K = 64..256, the bf16 stage-1 maps)."""
+    ms, fl, nl = prof
+    layers = arch_mod.conv_launch_bytes(arch_mod.SPECS[args.arch], args.res, args.res, ELEM_BYTES[dtype])
+    peak = MFMA_PEAK_TF[dtype] * 1e12
+    nlay = min(len(ms), len(layers))
+    # a conv with no launch of its own but bytes (bf16 bottleneck conv1 fused into the previous
+    # block's conv3 launch, pair1x1_bf16.hip; its FLOPs are in that record): its bytes less its
+    # input map (never re-read) join the launch it was fused into
+    eb = [[float(layers[i][0]), float(layers[i][1])] for i in range(nlay)]
+    for i in range(nlay):
+        if not nl[i] and layers[i][0]:
+            j = max((k for k in range(i) if nl[k]), default=None)
+            if j is not None:
+                eb[j][0] += layers[i][0] - layers[i][2]
+                eb[j][1] += layers[i][1]
+    t_meas = t_floor = t_hbm_layers = 0.0
+    n_hbm = n = 0
+    worst = None
+    for i in range(nlay):
+        if not nl[i]:
+            continue
+        pf, wb = eb[i]
+        t_m = float(fl[i]) / peak * 1e3
+        t_b = (frames * pf + int(nl[i]) * wb) / (HBM_PEAK_GBPS * 1e9) * 1e3
+        fl_i = max(t_m, t_b)
+        t_meas += float(ms[i])
+        t_floor += fl_i
+        n += 1
+        if t_b > t_m:
+            n_hbm += 1
+            t_hbm_layers += float(ms[i])
+        if worst is None or fl_i / float(ms[i]) < worst[1]:
+            worst = (i, fl_i / float(ms[i]), "hbm" if t_b > t_m else "mfma")
+    if not n:
+        return None
+    return {"frac": round(t_floor / t_meas, 4), "layers": n, "hbm_bound_layers": n_hbm,
+            "hbm_bound_time_share": round(t_hbm_layers / t_meas, 4),
+            "worst_layer": {"id": worst[0], "frac": round(worst[1], 4), "bound": worst[2]},
+            "hbm_peak": HBM_PEAK_GBPS, "mfma_peak": MFMA_PEAK_TF[dtype],
+            "definition": "sum over conv layers of max(FLOPs / MFMA peak, algorithmic bytes / HBM peak) "
+                          "/ sum of measured per-layer HIP-event times (layer ids: arch.conv_launch_bytes order)"}
 
 
 def print_layers(prof, tag):
@@ -212,6 +258,7 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
         out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, int(nl.sum()),
                                                                         int(nl[0])))
         out["traffic_source"] = src
+        out["per_layer_bound"] = layer_bounds(prof, dtype, args, arch_mod, frames)
     return out
 
 

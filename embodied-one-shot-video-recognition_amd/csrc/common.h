@@ -135,6 +135,25 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
                          LaunchInfo* info = nullptr);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
+
+// pair1x1_bf16.hip: a bottleneck's conv3 (1x1 64 -> 256 + residual, or + a folded stride-1
+// downsample reading x2 [M][64]) fused with the next block's conv1 (1x1 256 -> c1), bf16 NHWC
+struct Pair1x1Args {
+  const void* x;     // [M][64]   conv3 input
+  const void* x2;    // [M][cds]  downsample input (cds = 64) or nullptr
+  const void* res;   // [M][256]  residual (nullptr with the downsample)
+  const void* w3;    // [256][64 + cds] folded conv3 (+ downsample) weights
+  const float* b3;   // [256]
+  const void* w1;    // [c1][256] folded next conv1 weights
+  const float* b1;   // [c1]
+  void* y;           // [M][256]  conv3 output (the next block's residual)
+  void* z;           // [M][c1]   next conv1 output
+  long long M;       // pixels, a multiple of 64
+  int c1, cds;
+  LaunchInfo* plan;  // non-null: record the grid only
+};
+bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
+int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv

@@ -475,12 +475,68 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   return rc;
 }
 
+// bf16 bottleneck stage 1: block b's conv3 fused with block b+1's conv1 (pair1x1_bf16.hip) when
+// the shapes allow it.  EOSV_PAIR=0 (profiling build): unfused.
+static bool pair_enabled() {
+  static const bool v = env_switch("EOSV_PAIR", 1) != 0;
+  return v;
+}
+
+static bool pair_ok(const eosv_handle* h, const Block& b, const Block* nb, long long M) {
+  if (!pair_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || !nb || !nb->bottleneck) return false;
+  const Conv &c3 = b.c3, &n1 = nb->c1;
+  if (b.c2.stride != 1 || c3.kh != 1 || n1.kh != 1 || n1.stride != 1 || n1.cin != c3.cout) return false;
+  if (b.has_ds && !(b.fuse_ds && b.ds.stride == 1)) return false;
+  return pair1x1_bf16_ok(c3.cin, c3.cout, n1.cout, b.has_ds ? c3.kds : 0, M);
+}
+
+// conv3 of `b` (+ residual `res` or the folded downsample reading x2) -> y, and the next block's
+// conv1 on y -> z, in one launch; profiled as conv3's layer with both convs' FLOPs
+static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void* x, const void* x2, const void* res,
+                    void* y, void* z, long long M, hipStream_t s) {
+  Pair1x1Args p{};
+  p.x = x;
+  p.x2 = x2;
+  p.res = res;
+  p.w3 = b.c3.w;
+  p.b3 = b.c3.b;
+  p.w1 = nb.c1.w;
+  p.b1 = nb.c1.b;
+  p.y = y;
+  p.z = z;
+  p.M = M;
+  p.c1 = nb.c1.cout;
+  p.cds = x2 ? b.c3.kds : 0;
+  const double flops = 2.0 * M * ((double)b.c3.cout * (b.c3.cin + p.cds) + (double)nb.c1.cout * nb.c1.cin);
+  if (h->planning) {
+    LaunchInfo li{};
+    p.plan = &li;
+    const int prc = launch_pair1x1_bf16(p, s);
+    if (prc == EOSV_OK) add_plan_cost(h, li, flops);
+    return prc;
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->prof) {
+    e0 = prof_event(h);
+    e1 = prof_event(h);
+    if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
+    EOSV_HIP_CHECK(hipEventRecord(e0, s));
+  }
+  const int rc = launch_pair1x1_bf16(p, s);
+  if (h->prof && rc == EOSV_OK) {
+    EOSV_HIP_CHECK(hipEventRecord(e1, s));
+    h->recs.push_back({b.c3.id, e0, e1, flops});
+  }
+  return rc;
+}
+
 // Residual blocks [b0, b1) on x (B frames, hh x ww) using the 4-buffer set `bufs`.  The
 // output of each block lands in place of its residual buffer; when `dst` is given, the last
 // block writes there instead (its residual still comes from `bufs`).
 static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const* bufs, int B, int& hh,
                       int& ww, void* dst, void** xout, bool bf, hipStream_t s) {
   int rc;
+  bool c1_done = false;  // this block's conv1 output is already in fr[0] (fused into the previous pair)
   for (size_t bi = b0; bi < b1; ++bi) {
     const Block& b = h->blocks[bi];
     void* fr[3];
@@ -503,9 +559,20 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
       if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) return rc;
     } else {
-      if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
+      if (!c1_done && (rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
       if ((rc = run_conv(h, b.c2, fr[0], B, hh, ww, nullptr, fr[1], true, bf, s))) return rc;
-      if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) return rc;
+      // the next block's conv1 lands in its fr[0]: the first buffer that is not its input y
+      const Block* nb = bi + 1 < b1 ? &h->blocks[bi + 1] : nullptr;
+      void* z = nullptr;
+      for (int k = 0; k < 4 && !z; ++k)
+        if (bufs[k] != y) z = bufs[k];
+      const long long M = (long long)B * ho * wo;
+      c1_done = pair_ok(h, b, nb, M) && y != dst && z != x && z != fr[1];
+      if (c1_done) {
+        if ((rc = run_pair(h, b, *nb, fr[1], x2, res, y, z, M, s))) return rc;
+      } else if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) {
+        return rc;
+      }
     }
     x = y;
     hh = ho;
@@ -597,12 +664,14 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
       if ((rc = run_front(h, frames + s0 * fstride, nb, h->sbuf, dst, &x, bf, s))) return rc;
     }
     x = h->buf[1];
+    hh = h->front_hw[0];
+    ww = h->front_hw[1];
+    if ((rc = run_blocks(h, h->n_front, h->blocks.size(), x, h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
   } else {
-    if ((rc = run_front(h, frames, B, h->buf, nullptr, &x, bf, s))) return rc;
+    // every block in one pass, so that layer1's last conv3 can pair with layer2's first conv1
+    if ((rc = run_stem(h, frames, B, h->buf, bf, s))) return rc;
+    if ((rc = run_blocks(h, 0, h->blocks.size(), h->buf[1], h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
   }
-  hh = h->front_hw[0];
-  ww = h->front_hw[1];
-  if ((rc = run_blocks(h, h->n_front, h->blocks.size(), x, h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
   if (h->planning) return EOSV_OK;
   return launch_avgpool(x, B, hh * ww, h->D, feat, x3(h) ? 2 : bf ? 1 : 0, s);
 }

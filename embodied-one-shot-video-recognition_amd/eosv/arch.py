@@ -144,3 +144,47 @@ def conv_layer_bytes(spec: ResNetSpec, H: int = 224, W: int = 224, elem: int = 4
             h, w = ho, wo
             inplanes = cout
     return layers
+
+
+def conv_launch_bytes(spec: ResNetSpec, H: int = 224, W: int = 224, elem: int = 4):
+    """Algorithmic HBM bytes per conv launch as the native forward runs it, in the plan's layer-id
+    order (conv_layer_bytes' list, same indices): the fused stem + maxpool reads the caller's f32
+    NCHW frame and writes the pooled map; the downsample 1x1 is folded into its block's last conv
+    (csrc/eosv_api.hip), which then reads the downsample's input pixels instead of a residual map,
+    so the downsample's own entry is (0, 0, 0) and its weights move to that conv.  ``elem`` = bytes
+    per stored activation element (f32 4, bf16 2, f32x3 4: the (hi, lo) bf16 pair).  This is the
+    floor of each launch's traffic that the per-layer roofline (bench.py) prices at HBM peak.
+    Entries: (per-frame bytes, per-launch weight bytes, per-frame bytes of the input map) -- the
+    last is what a bf16 bottleneck conv1 fused with the previous conv3 (pair1x1_bf16.hip) saves."""
+    def out_hw(h, k, s, p):
+        return (h + 2 * p - k) // s + 1
+
+    h, w = out_hw(H, 7, 2, 3), out_hw(W, 7, 2, 3)
+    ph, pw = out_hw(h, 3, 2, 1), out_hw(w, 3, 2, 1)
+    layers = [(3 * H * W * 4 + ph * pw * 64 * elem, 64 * 147 * elem, 3 * H * W * 4)]
+    h, w = ph, pw
+    inplanes = 64
+    for li, (planes, n) in enumerate(zip((64, 128, 256, 512), spec.layers)):
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            cout = planes * spec.expansion
+            ho, wo = out_hw(h, 3, s, 1), out_hw(w, 3, s, 1)
+            ds = bi == 0 and (s != 1 or inplanes != cout)
+            # the last conv reads the residual, or (folded downsample) the block input at stride s
+            last_extra = ho * wo * inplanes if ds else ho * wo * cout
+            if spec.block == "basic":
+                layers.append(((h * w * inplanes + ho * wo * planes) * elem, planes * inplanes * 9 * elem, h * w * inplanes * elem))
+                layers.append(((ho * wo * planes + last_extra + ho * wo * cout) * elem, cout * planes * 9 * elem,
+                               ho * wo * planes * elem))
+            else:
+                layers.append(((h * w * inplanes + h * w * planes) * elem, planes * inplanes * elem, h * w * inplanes * elem))
+                layers.append(((h * w * planes + ho * wo * planes) * elem, planes * planes * 9 * elem, h * w * planes * elem))
+                layers.append(((ho * wo * planes + last_extra + ho * wo * cout) * elem, cout * planes * elem,
+                               ho * wo * planes * elem))
+            if ds:
+                pf, wb, pin = layers[-1]
+                layers[-1] = (pf, wb + cout * inplanes * elem, pin)
+                layers.append((0, 0, 0))
+            h, w = ho, wo
+            inplanes = cout
+    return layers

@@ -415,8 +415,82 @@ static int check_stem_pool_f32(int N, int H, int W, int every = 1) {
   return bad || rc ? 1 : 0;
 }
 
+// bottleneck 1x1 pair (pair1x1_bf16.hip) vs the unfused pair through launch_conv_bf16: conv3
+// (1x1 64 -> 256, + residual or + a folded stride-1 downsample) then the next block's conv1
+// (1x1 256 -> c1), both with folded-BN shifts and ReLU.  Same K order, same epilogue order:
+// both maps must be bit-identical.
+static int check_pair(int N, int H, int W, int c1, bool ds) {
+  const long long M = (long long)N * H * W;
+  const int K3 = ds ? 128 : 64;
+  unsigned s = 777;
+  auto fill = [&](std::vector<unsigned short>& v, float scale) {
+    for (auto& e : v) e = f2bf(frand(s) * scale);
+  };
+  std::vector<unsigned short> x(M * 64), x2(ds ? M * 64 : 1), res(M * 256), w3(256 * K3), w1((size_t)c1 * 256);
+  fill(x, 1.f); fill(x2, 1.f); fill(res, 1.f); fill(w3, 0.125f); fill(w1, 0.0625f);
+  std::vector<float> b3(256), b1(c1);
+  for (auto& v : b3) v = frand(s) * 0.5f;
+  for (auto& v : b1) v = frand(s) * 0.5f;
+  auto up = [](const void* p, size_t n) { void* d; hipMalloc(&d, n); hipMemcpy(d, p, n, hipMemcpyHostToDevice); return d; };
+  void *dx = up(x.data(), x.size() * 2), *dx2 = up(x2.data(), x2.size() * 2), *dr = up(res.data(), res.size() * 2);
+  void *dw3 = up(w3.data(), w3.size() * 2), *dw1 = up(w1.data(), w1.size() * 2);
+  float *db3 = (float*)up(b3.data(), b3.size() * 4), *db1 = (float*)up(b1.data(), b1.size() * 4);
+  void *y0, *z0, *y1, *z1, *dz;
+  hipMalloc(&y0, M * 512); hipMalloc(&y1, M * 512); hipMalloc(&z0, M * c1 * 2); hipMalloc(&z1, M * c1 * 2);
+  hipMalloc(&dz, 256); hipMemset(dz, 0, 256);
+  // unfused: conv3 (+ residual | + downsample K columns), then conv1
+  ConvArgs a{};
+  a.x = dx; a.w = dw3; a.bias = db3; a.res = ds ? nullptr : dr; a.y = y0;
+  a.N = N; a.H = H; a.W = W; a.Cin = 64; a.Ho = H; a.Wo = W; a.Cout = 256;
+  a.KH = a.KW = a.KWp = 1; a.stride = 1; a.pad = 0; a.K = K3; a.relu = 1; a.zero = dz; a.xcd = 1;
+  if (ds) { a.x2 = dx2; a.H2 = H; a.W2 = W; a.Cin2 = 64; a.stride2 = 1; a.K1 = 64; }
+  int rc = launch_conv_bf16(a, 0);
+  ConvArgs b{};
+  b.x = y0; b.w = dw1; b.bias = db1; b.res = nullptr; b.y = z0;
+  b.N = N; b.H = H; b.W = W; b.Cin = 256; b.Ho = H; b.Wo = W; b.Cout = c1;
+  b.KH = b.KW = b.KWp = 1; b.stride = 1; b.pad = 0; b.K = 256; b.relu = 1; b.zero = dz; b.xcd = 1;
+  rc |= launch_conv_bf16(b, 0);
+  Pair1x1Args p{};
+  p.x = dx; p.x2 = ds ? dx2 : nullptr; p.res = ds ? nullptr : dr; p.w3 = dw3; p.b3 = db3; p.w1 = dw1; p.b1 = db1;
+  p.y = y1; p.z = z1; p.M = M; p.c1 = c1; p.cds = ds ? 64 : 0;
+  rc |= launch_pair1x1_bf16(p, 0);
+  hipDeviceSynchronize();
+  std::vector<unsigned short> hy0(M * 256), hy1(M * 256), hz0(M * c1), hz1(M * c1);
+  hipMemcpy(hy0.data(), y0, M * 512, hipMemcpyDeviceToHost); hipMemcpy(hy1.data(), y1, M * 512, hipMemcpyDeviceToHost);
+  hipMemcpy(hz0.data(), z0, M * c1 * 2, hipMemcpyDeviceToHost); hipMemcpy(hz1.data(), z1, M * c1 * 2, hipMemcpyDeviceToHost);
+  long bady = 0, badz = 0;
+  double maxd = 0;
+  for (size_t i = 0; i < hy0.size(); ++i)
+    if (hy0[i] != hy1[i]) ++bady, maxd = std::max(maxd, (double)fabs(bf2f(hy0[i]) - bf2f(hy1[i])));
+  for (size_t i = 0; i < hz0.size(); ++i)
+    if (hz0[i] != hz1[i]) ++badz, maxd = std::max(maxd, (double)fabs(bf2f(hz0[i]) - bf2f(hz1[i])));
+  // the unfused maps themselves against double on the bf16 operands (a few pixels)
+  double maxerr = 0;
+  for (long long m = 0; m < M; m += M / 7 + 1)
+    for (int o = 0; o < 256; o += 5) {
+      double acc = b3[o];
+      for (int k = 0; k < 64; ++k) acc += (double)bf2f(x[m * 64 + k]) * bf2f(w3[o * K3 + k]);
+      if (ds) for (int k = 0; k < 64; ++k) acc += (double)bf2f(x2[m * 64 + k]) * bf2f(w3[o * K3 + 64 + k]);
+      else acc += bf2f(res[m * 256 + o]);
+      acc = std::max(acc, 0.0);
+      maxerr = std::max(maxerr, fabs(acc - bf2f(hy0[m * 256 + o])) / (1.0 + fabs(acc)));
+    }
+  const bool fail = rc || bady || badz || maxerr > 1e-2;
+  printf("%s pair1x1 bf16 N%d H%d W%d c1 %d ds%d rc=%d differing y %ld z %ld (max %.3e) unfused maxerr %.3e\n",
+         fail ? "FAIL" : "ok  ", N, H, W, c1, ds ? 1 : 0, rc, bady, badz, maxd, maxerr);
+  for (void* q : {dx, dx2, dr, dw3, dw1, (void*)db3, (void*)db1, y0, y1, z0, z1, dz}) hipFree(q);
+  return fail ? 1 : 0;
+}
+
 int main() {
   int fails = 0;
+  // R50 layer1 pairs: block 1/2 (residual, c1 64), block 0 (downsample), layer1 -> layer2 (c1 128);
+  // 700 images = 34300 tiles (~134 per workgroup), 64-wide maps (R101 @ 256)
+  fails += check_pair(700, 56, 56, 64, false);
+  fails += check_pair(9, 56, 56, 64, true);
+  fails += check_pair(9, 56, 56, 128, false);
+  fails += check_pair(5, 64, 64, 64, false);
+  fails += check_pair(1, 8, 8, 64, true);  // one tile: the grid is smaller than the CU count
   fails += check_stem_pool(2, 224, 224);
   fails += check_stem_pool(3, 100, 86);  // ragged: partial last column tile, odd pooled sizes
   fails += check_stem_pool(2, 64, 48);
