@@ -316,3 +316,48 @@ def test_train_network_steplr_matches_torch_schedule():
                 s2.step()
                 l1, l2 = network_train.TrainNetwork.lr_at(tn, epoch)
                 assert abs(l1 - o1.param_groups[0]["lr"]) <= 1e-12 and abs(l2 - o2.param_groups[0]["lr"]) <= 1e-12
+
+
+def test_conv_launch_bytes_and_per_layer_bound():
+    """bench.py's per-layer roofline: arch.conv_launch_bytes follows the native plan's layer ids
+    (a folded downsample's entry is empty, its weights on the block's last conv), and
+    layer_bounds prices each launch at max(MFMA, HBM) with a fused conv1's bytes (less its
+    input map) moved onto the launch it was fused into."""
+    import types
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(GOLDEN)))  # the repo root: bench.py
+    import bench
+    from eosv import arch
+
+    spec = arch.SPECS["resnet50"]
+    L = arch.conv_launch_bytes(spec, 224, 224, 2)
+    assert len(L) == len(arch.conv_layer_bytes(spec, 224, 224, 2, True))
+    # stem: f32 frame in, pooled bf16 map out
+    assert L[0][0] == 3 * 224 * 224 * 4 + 56 * 56 * 64 * 2
+    # layer1 block 0: conv3 reads its 64-ch input and the downsample's 64-ch input, writes 256 ch
+    assert L[3][0] == (56 * 56 * 64 + 56 * 56 * 64 + 56 * 56 * 256) * 2
+    assert L[3][1] == (256 * 64 + 256 * 64) * 2 and L[4] == (0, 0, 0)
+    # block 1 conv3: + the 256-ch residual
+    assert L[7][0] == (56 * 56 * 64 + 2 * 56 * 56 * 256) * 2
+    # conv1 of block 1: input map 256 ch
+    assert L[5][2] == 56 * 56 * 256 * 2
+    frames = 1000
+    n = len(L)
+    ms, fl, nl = np.zeros(n), np.zeros(n), np.zeros(n)
+    for i in range(n):  # every conv launched once, except the downsamples and block 2's conv1 (fused)
+        if L[i][0] and i != 8:
+            nl[i], ms[i] = 1, 1.0
+    fl[7] = 2 * frames * 56 * 56 * (256 * 64 + 64 * 256)  # conv3 + the fused next conv1
+    args = types.SimpleNamespace(arch="resnet50", res=224)
+    out = bench.layer_bounds((ms, fl, nl), "bf16", args, arch, frames)
+    hbm = bench.HBM_PEAK_GBPS * 1e9
+    floors = []
+    for i in range(n):
+        if not nl[i]:
+            continue
+        b = frames * L[i][0] + L[i][1]
+        if i == 7:  # the fused conv1's bytes, less its input map (never re-read)
+            b += frames * (L[8][0] - L[8][2]) + L[8][1]
+        floors.append(max(b / hbm * 1e3, fl[i] / (bench.MFMA_PEAK_TF["bf16"] * 1e12) * 1e3))
+    assert out["layers"] == int(nl.sum()) and out["hbm_bound_layers"] == int(nl.sum())
+    assert abs(out["frac"] - sum(floors) / ms.sum()) < 1e-4
