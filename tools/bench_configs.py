@@ -39,7 +39,7 @@ def config3(args):
     utils.EPISODE_NUMS["test"] = args.episodes
     tn = network_test.TestNetwork(os.path.join(td, "acc.txt"), "resnet50", "protonet", True)
     tn.mymodel.compute_dtype = args.dtype
-    tn.mymodel.max_frames = 1024
+    tn.mymodel.max_frames = args.max_frames or 4096  # r02: 4096 +6 % over 1024 (tools/mf_configs.sh)
     import io
     import contextlib
 
@@ -146,7 +146,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-episodes", type=int, default=0, help="config 3: oracle episodes for cpu_baseline")
-    ap.add_argument("--max-frames", type=int, default=2048, help="backbone chunk (configs 4 / 5)")
+    ap.add_argument("--max-frames", type=int, default=0, help="backbone chunk (default: 4096 config 3, 2048 configs 4 / 5)")
     args = ap.parse_args()
     if args.config == 3:
         print(json.dumps(config3(args)), flush=True)
@@ -158,7 +158,7 @@ def main():
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), *shape, "--dtype", args.dtype,
            "--episodes-per-step", str(args.episodes), "--steps", "2", "--secondary-dtype", "",
            "--cpu-baseline-sec", "10",
-           "--max-frames", str(args.max_frames), "--config-label", f"BASELINE configs[{args.config - 1}]"]
+           "--max-frames", str(args.max_frames or 2048), "--config-label", f"BASELINE configs[{args.config - 1}]"]
     sys.exit(subprocess.call(cmd))
 
 
