@@ -71,8 +71,11 @@ class _NativeResNet(nn.Module):
     #: arithmetic of the native conv stack: 'f32' (exact-f32 MFMA, reference parity), 'f32x3'
     #: (f32-accurate split-bf16 MFMA, within 1e-4 of f32, ~2.4x faster) or 'bf16'
     compute_dtype = "f32"
-    #: frames per internal chunk of the native handle (workspace size)
-    max_frames = 256
+    #: frames per internal chunk of the native handle (workspace size: 4 activation buffers of
+    #: max_frames x the largest map, e.g. R50 bf16 6.4 GB, R50 f32 26 GB at 2048).  Grids of a
+    #: few hundred frames leave CUs idle (R50 layer 3 at 256 frames: 196 tiles on 256 CUs); the
+    #: episode drivers batch thousands of frames per call (config 3: +6 % from 1024 to 4096)
+    max_frames = 2048
 
     def __init__(self, num_classes):
         super().__init__()
