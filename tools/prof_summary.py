@@ -86,7 +86,7 @@ if bench:
     open(f"{dst}/{tag}_bench.json", "w").write(json.dumps(bench) + "\n")
 
 # conv-family HBM traffic per launch (read by bench.py into roofline.traffic)
-FAMILIES = {"f32": ("conv_f32",), "bf16": ("conv_bf16", "conv_rows_bf16", "stem_pool_bf16"),
+FAMILIES = {"f32": ("conv_f32",), "bf16": ("conv_bf16", "conv_rows_bf16", "stem_pool_bf16", "pair1x1_bf16"),
             "f32x3": ("conv_bf16", "stem_pool_x3")}
 
 
