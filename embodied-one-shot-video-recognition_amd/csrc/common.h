@@ -130,9 +130,11 @@ bool stem_pool_x3_ok(int H, int W);  // stem_pool_bf16.hip: EOSV_F32X3 split-bf1
 int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w, const float* bias, void* y,
                         hipStream_t s, LaunchInfo* info = nullptr);
 bool stem_pool_f32_ok(int H, int W);  // stem_pool_f32.hip: the same for f32
+bool stem_pool_f32_direct_ok(int H, int W);  // ... reading the f32 NCHW frames (W % 4 == 0, W <= 256)
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                          hipStream_t s, bool split = false,  // split: y in the EOSV_F32X3 (hi, lo) layout
-                         LaunchInfo* info = nullptr);
+                         LaunchInfo* info = nullptr,
+                         const float* frames = nullptr);  // non-null: DIRECT (pack unused, may be null)
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 

@@ -599,9 +599,10 @@ static int run_stem(eosv_handle* h, const float* frames, int B, void* const* buf
   const bool x3stem = x3(h) && direct && x3_split_stem && h->stem_x3.w && stem_pool_x3_ok(H, W);
   const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W, direct) : stem_pool_f32_ok(H, W));
   if (x3(h) && !fused && !x3stem) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
-  // the bf16 fused stem reads the f32 NCHW frames itself (no pack pass)
+  // the bf16 and f32 fused stems read the f32 NCHW frames themselves (no pack pass)
   const bool direct_bf = fused && sbf && direct;
-  if (!direct_bf && !x3stem && !h->planning &&
+  const bool direct_f32 = fused && !sbf && direct && stem_pool_f32_direct_ok(H, W);
+  if (!direct_bf && !direct_f32 && !x3stem && !h->planning &&
       (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s)))
     return rc;
   if (h->planning && (fused || x3stem)) {
@@ -609,7 +610,8 @@ static int run_stem(eosv_handle* h, const float* frames, int B, void* const* buf
     if ((rc = x3stem ? launch_stem_pool_x3(frames, B, H, W, h->stem_x3.w, h->stem_x3.b, bufs[1], s, &li)
               : sbf  ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
                                              direct_bf ? frames : nullptr, &li)
-                     : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s, x3(h), &li)))
+                     : launch_stem_pool_f32(direct_f32 ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
+                                            x3(h), &li, direct_f32 ? frames : nullptr)))
       return rc;
     add_plan_cost(h, li, 2.0 * B * h->hs * h->ws * 64 * 147);
   } else if (fused || x3stem) {
@@ -624,7 +626,8 @@ static int run_stem(eosv_handle* h, const float* frames, int B, void* const* buf
     if ((rc = x3stem ? launch_stem_pool_x3(frames, B, H, W, h->stem_x3.w, h->stem_x3.b, bufs[1], s)
               : sbf  ? launch_stem_pool_bf16(direct_bf ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
                                              direct_bf ? frames : nullptr)
-                     : launch_stem_pool_f32(h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s, x3(h))))
+                     : launch_stem_pool_f32(direct_f32 ? nullptr : h->pack, B, H, W, h->stem.w, h->stem.b, bufs[1], s,
+                                            x3(h), nullptr, direct_f32 ? frames : nullptr)))
       return rc;
     if (h->prof) {
       EOSV_HIP_CHECK(hipEventRecord(e1, s));

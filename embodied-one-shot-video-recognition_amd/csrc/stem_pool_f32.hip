@@ -71,7 +71,15 @@ __device__ __forceinline__ float row_ror1(float v) {
 // x: padded f32 RGB [N][H+6][Wp][3] (stem_row_pixels), w: [64][176] f32, bias [64] f32,
 // y: [N][Hq][Wq][64] f32 (pooled).  Grid = N images, block = 256 threads, NT = ceil(Ws / 16).
 // SPLIT (EOSV_F32X3): y is [N][Hq][Wq][128] bf16, (hi, lo) of each pooled f32 value.
-template <bool SPLIT, int NT>
+// DIRECT: x is the caller's f32 NCHW frames [N][3][H][W] (W % 4 == 0, W <= 256) instead of the
+// padded pack: step py LDS-DMAs the input rows of step py + 2's prefetch as 12 plane rows into a
+// staging area (wave g: row g's 3 planes), and wave g interleaves its row into the ring at the
+// start of step py + 1, zero padding included (the pack's layout, the same f32 values:
+// bit-identical results); the first rows are loaded directly.  No pack pass: its 602 KB read +
+// 635 KB write per frame are gone.
+constexpr int SPF_SROW = 264;  // staged plane row (floats): 3 + one 1-KiB DMA piece (W <= 256), 16-B rows
+
+template <bool SPLIT, int NT, bool DIRECT = false>
 __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ bias, void* y, int H,
@@ -90,7 +98,8 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
   const int RF = spf_row_floats(Wp);  // ring row stride (floats)
   const int Hpad = H + 6;
   float* ring = spf_smem;
-  const float* ximg = x + (long long)img * Hpad * Wp * 3;
+  const float* ximg = x + (long long)img * (DIRECT ? 3LL * H * W : (long long)Hpad * Wp * 3);
+  float* stg = spf_smem + SPF_RING * RF + SPF_SLACK;  // DIRECT: [row 4][plane 3][SPF_SROW]
 
   // A fragments: W[16g + r16][k = 4s + q], dense k -> uploaded [kh][24] column
   float wa[SPF_STEPS];
@@ -105,6 +114,47 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
   // past the padded image are clamped (their results are discarded)
   const int row_chunks = RF / 4;
   const int ppr = (row_chunks + 63) / 64;
+  // DIRECT: padded input row pr -> ring slot pr % 13, interleaved RGB, zero padding
+  auto direct_rows = [&](int r0, int nrows) {
+    for (int t = tid; t < nrows * Wp; t += SPF_NT) {
+      const int rr = t / Wp, pp = t - Wp * (t / Wp);
+      const int yy = r0 + rr - 3, xx = pp - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      float* d = ring + ((r0 + rr) % SPF_RING) * RF + 3 * pp;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) d[c] = ok ? ximg[((long long)c * H + yy) * W + xx] : 0.f;
+    }
+  };
+  // wave g stages padded row r0 + g (its 3 plane rows) and later converts that row itself: the
+  // staging never crosses waves, so a wave waits only for its own DMA (no extra barrier).  A plane
+  // row lands 3 floats in, so staged index = padded column: lane k converts padded columns
+  // 4k .. 4k + 3 with 3 aligned 16-B reads and 3 16-B ring writes (12 interleaved floats).
+  auto stage_direct = [&](int r0) {
+    const int yy = min(max(r0 + g - 3, 0), H - 1);  // out-of-image rows: zeroed at conversion
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (lane < W / 4) dma16(ximg + ((long long)c * H + yy) * W + 4 * lane, stg + (g * 3 + c) * SPF_SROW + 3);
+  };
+  auto convert = [&](int r0) {
+    const bool rowin = (unsigned)(r0 + g - 3) < (unsigned)H;
+    float* d0 = ring + ((r0 + g) % SPF_RING) * RF;
+    for (int k = lane; 4 * k < Wp; k += 64) {
+      f32x4 v[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = *(const f32x4*)(stg + (g * 3 + c) * SPF_SROW + 4 * k);
+      float o[12];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = rowin && (unsigned)(4 * k + e - 3) < (unsigned)W;  // padding columns: 0
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[3 * e + c] = ok ? v[c][e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (12 * k + 4 * i < RF)  // the last group's tail past the row is not written
+          *(f32x4*)(d0 + 12 * k + 4 * i) = f32x4{o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+    }
+  };
   auto stage = [&](int r0, int nrows) {
     for (int p = g; p < nrows * ppr; p += 4) {
       const int rr = p / ppr, pc = p - ppr * (p / ppr);
@@ -148,13 +198,19 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
 #pragma unroll
   for (int k = 0; k < NT; ++k) prev[k] = f32x4{NEG, NEG, NEG, NEG};
   if (py0 == 0) {
-    stage(0, SPF_RING);
+    if constexpr (DIRECT)
+      direct_rows(0, SPF_RING);
+    else
+      stage(0, SPF_RING);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else {
     // a band below the top starts with stem row 2 py0 - 1 (input rows 4 py0 - 2 .. 4 py0 + 4);
     // rows up to 4 py0 + 8 are the first step's
-    stage(4 * py0 - 2, 11);
+    if constexpr (DIRECT)
+      direct_rows(4 * py0 - 2, 11);
+    else
+      stage(4 * py0 - 2, 11);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     f32x4 a0[NT];
@@ -167,13 +223,28 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
     // every wave is done with rows 4 py0 - 2, 4 py0 - 1 before the first step's DMA reuses their slots
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
+    // DIRECT: the first step's prefetch rows 4 py0 + 9 .. + 12 directly (read from step py0 + 1 on,
+    // after that step's barrier)
+    if constexpr (DIRECT)
+      if (py0 + 1 < py1) direct_rows(4 * py0 + 9, 4);
   }
   float* yimg = (float*)y + (long long)img * Hq * Wq * 64;
   unsigned short* ysp = (unsigned short*)y + (long long)img * Hq * Wq * 128;
   const bool even = !(r16 & 1);
 
   for (int py = py0; py < py1; ++py) {
-    if (py + 1 < py1) stage(4 * py + 9, 4);
+    if constexpr (DIRECT) {
+      // rows 4py + 9 .. + 12 (read from step py + 1 on): staged during step py - 1 and landed by
+      // its end-of-step wait; step py0's came directly in the prologue.  Then this wave's staging
+      // slot takes the next step's row.
+      if (py > py0 && py + 1 < py1) convert(4 * py + 9);
+      if (py + 2 < py1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own staging reads done before the DMA rewrites it
+        stage_direct(4 * py + 13);
+      }
+    } else if (py + 1 < py1) {
+      stage(4 * py + 9, 4);
+    }
     f32x4 a1[NT], a2[NT];
     stem_row(2 * py, a1);
     stem_row(2 * py + 1, a2);
@@ -250,42 +321,54 @@ bool stem_pool_f32_ok(int H, int W) {
   return H >= 8 && W >= 8 && (Ws + 15) / 16 <= SPF_MAX_TILES;
 }
 
-template <bool SPLIT, int NT>
-static void launch_nt(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
+template <bool SPLIT, int NT, bool DIRECT>
+static void launch_nt(const void* x, int B, int H, int W, const void* w, const float* bias, void* y,
                       hipStream_t s, size_t lds, int Hs, int Ws, int Hq, int Wq, int bands) {
-  hipLaunchKernelGGL((stem_pool_f32_kernel<SPLIT, NT>), dim3(B * bands), dim3(SPF_NT), lds, s, (const float*)pack,
+  hipLaunchKernelGGL((stem_pool_f32_kernel<SPLIT, NT, DIRECT>), dim3(B * bands), dim3(SPF_NT), lds, s, (const float*)x,
                      (const float*)w, bias, y, H, W, Hs, Ws, Hq, Wq, bands);
 }
 
-template <bool SPLIT>
-static void launch_split(int nt, const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
+template <bool SPLIT, bool DIRECT>
+static void launch_split(int nt, const void* x, int B, int H, int W, const void* w, const float* bias, void* y,
                          hipStream_t s, size_t lds, int Hs, int Ws, int Hq, int Wq, int bands) {
   switch (nt) {
 #define EOSV_SPF_NT(n) \
   case n:              \
-    return launch_nt<SPLIT, n>(pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
+    return launch_nt<SPLIT, n, DIRECT>(x, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
     EOSV_SPF_NT(1) EOSV_SPF_NT(2) EOSV_SPF_NT(3) EOSV_SPF_NT(4) EOSV_SPF_NT(5) EOSV_SPF_NT(6) EOSV_SPF_NT(7)
     EOSV_SPF_NT(8)
 #undef EOSV_SPF_NT
   }
 }
 
+bool stem_pool_f32_direct_ok(int H, int W) { return stem_pool_f32_ok(H, W) && W % 4 == 0 && W <= 256; }
+
+// pack: the padded RGB rows (pack_rgb_pad), or nullptr with `frames` = the f32 NCHW input (DIRECT)
 int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
-                         hipStream_t s, bool split, LaunchInfo* info) {
+                         hipStream_t s, bool split, LaunchInfo* info, const float* frames) {
   const int Hs = (H + 6 - 7) / 2 + 1, Ws = (W + 6 - 7) / 2 + 1;
   const int Hq = (Hs + 2 - 3) / 2 + 1, Wq = (Ws + 2 - 3) / 2 + 1;
   const int nt = (Ws + 15) / 16;
   if (B <= 0) return EOSV_OK;
-  if (!stem_pool_f32_ok(H, W)) return set_error("stem_pool_f32: unsupported frame size"), EOSV_ERR_UNSUPPORTED;
-  const size_t lds = (size_t)(SPF_RING * spf_row_floats(stem_row_pixels(W, 3)) + SPF_SLACK) * 4;
+  if (!stem_pool_f32_ok(H, W) || (frames && !stem_pool_f32_direct_ok(H, W)))
+    return set_error("stem_pool_f32: unsupported frame size"), EOSV_ERR_UNSUPPORTED;
+  const size_t lds = (size_t)(SPF_RING * spf_row_floats(stem_row_pixels(W, 3)) + SPF_SLACK +
+                              (frames ? 12 * SPF_SROW : 0)) * 4;
   if (lds > 163840) return set_error("stem_pool_f32: rows too wide for LDS"), EOSV_ERR_UNSUPPORTED;
-  static const int occ = kernel_occupancy((const void*)stem_pool_f32_kernel<false, 7>, SPF_NT, lds);
+  static const int occ_pack = kernel_occupancy((const void*)stem_pool_f32_kernel<false, 7>, SPF_NT, lds);
+  static const int occ_direct = kernel_occupancy((const void*)stem_pool_f32_kernel<false, 7, true>, SPF_NT, lds);
+  const int occ = frames ? occ_direct : occ_pack;
   const int bands = spf_bands(B, Hq, occ);
   if (info) return record_launch(info, B * bands, occ);
-  if (split)
-    launch_split<true>(nt, pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
+  const void* x = frames ? (const void*)frames : pack;
+  if (split && frames)
+    launch_split<true, true>(nt, x, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
+  else if (split)
+    launch_split<true, false>(nt, x, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
+  else if (frames)
+    launch_split<false, true>(nt, x, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
   else
-    launch_split<false>(nt, pack, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
+    launch_split<false, false>(nt, x, B, H, W, w, bias, y, s, lds, Hs, Ws, Hq, Wq, bands);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

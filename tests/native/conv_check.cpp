@@ -410,9 +410,32 @@ static int check_stem_pool_f32(int N, int H, int W, int every = 1) {
           maxerr = fmax(maxerr, e);
         }
   }
-  printf("%s stem_pool f32 N%d H%d W%d rc=%d maxerr %.3e bad %ld\n", bad ? "FAIL" : "ok  ", N, H, W, rc, maxerr, bad);
+  // DIRECT (the f32 NCHW frames, no pack): the same values, so bit-identical to the pack run
+  long dbad = 0;
+  int rc2 = 0;
+  const bool direct = stem_pool_f32_direct_ok(H, W);
+  if (direct) {
+    std::vector<float> fr((size_t)N * 3 * H * W);
+    for (int n = 0; n < N; ++n)
+      for (int c = 0; c < 3; ++c)
+        for (int i = 0; i < H; ++i)
+          for (int j = 0; j < W; ++j)
+            fr[(((size_t)n * 3 + c) * H + i) * W + j] = x[(((size_t)n * Hp + i + pad) * Wp + j + pad) * 3 + c];
+    float *dfr, *dy2;
+    hipMalloc(&dfr, fr.size() * 4); hipMalloc(&dy2, ny * 4);
+    hipMemcpy(dfr, fr.data(), fr.size() * 4, hipMemcpyHostToDevice);
+    hipMemset(dy2, 0xff, ny * 4);
+    rc2 = launch_stem_pool_f32(nullptr, N, H, W, dw, db, dy2, 0, false, nullptr, dfr);
+    hipDeviceSynchronize();
+    std::vector<float> y2(ny);
+    hipMemcpy(y2.data(), dy2, ny * 4, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < ny; ++i) dbad += memcmp(&y[i], &y2[i], 4) != 0;
+    hipFree(dfr); hipFree(dy2);
+  }
+  printf("%s stem_pool f32 N%d H%d W%d rc=%d maxerr %.3e bad %ld%s\n", bad || dbad || rc2 ? "FAIL" : "ok  ", N, H, W,
+         rc, maxerr, bad, direct ? (dbad || rc2 ? " direct differs" : " direct identical") : "");
   hipFree(dx); hipFree(dw); hipFree(dy); hipFree(db);
-  return bad || rc ? 1 : 0;
+  return bad || rc || dbad || rc2 ? 1 : 0;
 }
 
 // bottleneck 1x1 pair (pair1x1_bf16.hip) vs the unfused pair through launch_conv_bf16: conv3
