@@ -180,6 +180,20 @@ def test_backbone_f32_other_archs(name, res):
     bb.close()
 
 
+def test_backbone_f32_pack_stem_width():
+    """A frame width the DIRECT f32 stem does not take (W % 4 != 0): the pack_rgb_pad + LDS-DMA
+    stem path, non-square frames, vs the oracle."""
+    sd = synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0)
+    bb = engine.Backbone("resnet18", "f32", 96, 90, max_frames=4)
+    bb.load_state_dict(sd)
+    x = torch.randn(3, 3, 96, 90, generator=torch.Generator().manual_seed(12))
+    out = bb.forward(x.cuda()).cpu().numpy()
+    with torch.no_grad():
+        ref = resnet_ref.build_model("resnet18", sd)(x)[0].numpy()
+    assert _rel_err(out, ref) < 2e-5
+    bb.close()
+
+
 def test_normalize_frames_bit_exact_vs_host_transform():
     """Fused ingest kernel == the host restatement of CenterCrop/ToTensor/Normalize."""
     from eosv import frames as fr
