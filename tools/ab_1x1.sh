@@ -1,3 +1,6 @@
+#!/bin/bash
+# r02 experiment record: 128x128 tiles for the R50 bf16 1x1 convs, selected by
+# EOSV_BF16_1X1 in a build that had it; not kept, so on the current tree the switch is ignored.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for v in 0 1 2 0 1 2; do

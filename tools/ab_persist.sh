@@ -1,3 +1,7 @@
+#!/bin/bash
+# r02 experiment record: A/B of a persistent 256x256 bf16 conv selected by
+# EOSV_BF16_PERSIST in a build that had it; the variant was not kept, so on the current tree the
+# switch is ignored and both arms run the same kernel.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 # 1. regression: the restructured default kernel vs the committed build (R50 bf16, R18 bf16)
