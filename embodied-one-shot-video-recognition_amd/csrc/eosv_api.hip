@@ -588,6 +588,16 @@ static bool stem_pool_fused(bool bf) {
   return bf ? vb : vf;
 }
 
+// Whether the stem path launches pack_rgb_pad (run_stem's decision): only then does eosv_create
+// size the padded-RGB pack buffer for max_frames (2.6 GB f32 / 1.3 GB bf16 at 4096 frames of 224²)
+static bool stem_needs_pack(const eosv_handle* h) {
+  const int H = h->d.height, W = h->d.width;
+  static const bool direct = env_switch("EOSV_STEM_DIRECT", 1) != 0;
+  const bool sbf = stem_bf(h);
+  const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W, direct) : stem_pool_f32_ok(H, W));
+  return !(fused && direct && (sbf || stem_pool_f32_direct_ok(H, W)));
+}
+
 // stem -> maxpool for frames [0, B) of `frames`, output into bufs[1]
 static int run_stem(eosv_handle* h, const float* frames, int B, void* const* bufs, bool bf, hipStream_t s) {
   const int H = h->d.height, W = h->d.width;
@@ -602,6 +612,7 @@ static int run_stem(eosv_handle* h, const float* frames, int B, void* const* buf
   // the bf16 and f32 fused stems read the f32 NCHW frames themselves (no pack pass)
   const bool direct_bf = fused && sbf && direct;
   const bool direct_f32 = fused && !sbf && direct && stem_pool_f32_direct_ok(H, W);
+  // (direct_bf || direct_f32) == !stem_needs_pack(h): otherwise the pack buffer is a stub
   if (!direct_bf && !direct_f32 && !x3stem && !h->planning &&
       (rc = launch_pack_rgb_pad(frames, B, H, W, h->stem.pad, h->pack, sbf, s)))
     return rc;
@@ -759,7 +770,9 @@ int eosv_create(const eosv_desc* desc, eosv_handle** out) {
   const size_t elt = act_bytes(h);
   const size_t F = (size_t)desc->max_frames;
   // + 256 B: the fused bf16 stem's DMA reads up to 12 B before a row (stem_pool_bf16.hip)
-  const size_t pack_bytes = stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * (stem_bf(h) ? 2 : 4) + 256;
+  const size_t pack_bytes =
+      rc || !stem_needs_pack(h) ? 256
+                                : stem_input_elems((int)F, desc->height, desc->width, h->stem.pad) * (stem_bf(h) ? 2 : 4) + 256;
   void* pack_base = nullptr;
   if (!rc) rc = dmalloc(h, &pack_base, pack_bytes);
   // zero borders of the padded stem input: written once here, the packer only fills interiors
