@@ -155,14 +155,16 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     bb.profile(False)
     bb.close()
     from eosv import dist as edist
-    return edist.max_over_ranks(elapsed), torch.cat(preds), prof, emb.cpu().numpy()
+    run_timed.per_rank_elapsed = edist.gather_values(elapsed)
+    return max(run_timed.per_rank_elapsed), torch.cat(preds), prof, emb.cpu().numpy()
 
 
 def measured_traffic(dtype, key):
     """HBM bytes per conv launch from the newest profiles/<tag>_traffic.json (written by
     tools/prof_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-    same command); EOSV_TRAFFIC_PROFILE names a specific file.  None if there is none or it was
-    measured on another workload (key = arch@HxW)."""
+    same command); EOSV_TRAFFIC_PROFILE names a specific file.  None if there is none, it was
+    measured on another workload (key = arch@HxW), or on other kernel sources than this tree's
+    (its src_sha16 differs from eosv._lib.source_digest())."""
     import glob
     path = os.environ.get("EOSV_TRAFFIC_PROFILE") or \
         (sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))) or [None])[-1]
@@ -170,6 +172,10 @@ def measured_traffic(dtype, key):
         return None, None
     d = json.load(open(path))
     if dtype not in d or d.get("key") != key:
+        return None, None
+    from eosv._lib import source_digest
+    if d.get("src_sha16") != source_digest():
+        # measured on other kernels than the ones in this tree: never attach a stale figure
         return None, None
     return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
 
@@ -249,7 +255,7 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
            "kernel": f"conv_{dtype}_kernel family: all {int(nl.sum())} conv launches of the timed region, "
                      f"summed algorithmic FLOPs / summed HIP-event durations on the launch stream"}
     if dtype == "f32x3":
-        out["kernel"] += ("; f32x3 = conv_bf16 kernels on the split (hi, lo, hi) layout + the split-bf16 fused "
+        out["kernel"] += ("; f32x3 = conv_bf16 kernels on the split (hi, lo) layout + the split-bf16 fused "
                           "stem (stem_pool_x3_cb_kernel), algorithmic (f32) FLOPs; peak = bf16 dense peak / 3")
     if args is not None and nl.sum() > 0:
         tr, src = measured_traffic(dtype, f"{args.arch}@{args.res}x{args.res}")
@@ -314,7 +320,9 @@ def main():
     timed_idx = mine_idx[args.warmup * E:]
 
     elapsed, pred, prof, emb = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
-    clips = edist.sum_over_ranks(sum(d.batch.n_clips for d in batches[args.warmup:]))
+    per_rank_elapsed = run_timed.per_rank_elapsed
+    per_rank_clips = [int(v) for v in edist.gather_values(sum(d.batch.n_clips for d in batches[args.warmup:]))]
+    clips = sum(per_rank_clips)
     frames_rank = sum(d.batch.n_frames for d in batches[args.warmup:])
     frames = edist.sum_over_ranks(frames_rank)
     # (episode, prediction) pairs: ONE all-gather over xGMI (RCCL) after the timed region
@@ -352,6 +360,9 @@ def main():
             "value": round(clips / elapsed, 2),  # whole job: all ranks' clips / max-over-ranks time
             "unit": "clips/s",
             "value_per_gpu": round(clips / elapsed / world, 2),
+            # the metric string is BASELINE.json's; 'value' is the driver contract's whole-job figure
+            "value_semantics": "value = all ranks' clips / max-over-ranks time (whole job over n_gpus); "
+                               "the metric's per-GPU figure is value_per_gpu = value / n_gpus",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -370,6 +381,11 @@ def main():
                        "episodes_per_step_per_gpu": E, "episodes_timed": E * args.steps * world,
                        "frames_per_clip": T, "parallelism": f"episode-sharded dp{world}"},
             "frames_per_s": round(frames / elapsed, 1),
+            # self-verifying multi-rank record: what the process group reports, and every rank's share
+            "dist": dict(edist.describe(), launched_world_size=world,
+                         per_rank_clips=per_rank_clips,
+                         per_rank_elapsed_s=[round(v, 6) for v in per_rank_elapsed],
+                         collective="all_gather of (episode, prediction) int64 pairs after the timed region"),
             "episode_acc": round(acc, 4),
             "roofline": rl,
             "cpu_baseline": None,

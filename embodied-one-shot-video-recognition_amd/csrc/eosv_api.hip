@@ -696,20 +696,20 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
 // dry-run forward's FLOPs divided by each launch's wave efficiency (add_plan_cost); B frames are
 // split into n - 1 chunks of c frames and a last one (n = the fewest chunks max_frames allows,
 // or one more), choosing c by that price.  Prices are computed once per handle for every chunk
-// size, plans once per frame count.  EOSV_CHUNK_PLAN=0 (profiling build): equal chunks.
+// size the planner tries (lazily), plans once per frame count.  EOSV_CHUNK_PLAN=0 (profiling build): equal chunks.
 static double price_chunk(eosv_handle* h, int F) {
-  if (h->chunk_cost.empty()) {
-    h->chunk_cost.assign((size_t)h->d.max_frames + 1, 0.0);
-    for (int f = 1; f <= h->d.max_frames; ++f) {
-      h->planning = true;
-      h->plan_cost = 0.0;
-      // any non-null frame pointer: the launchers choose their kernel by it and record the grid
-      const int rc = forward_chunk(h, (const float*)h->zero, f, nullptr, nullptr);
-      h->planning = false;
-      h->chunk_cost[f] = rc ? 1e300 : h->plan_cost;
-    }
+  // priced lazily, one dry run per chunk size the planner asks for (-1 = not yet priced)
+  if (h->chunk_cost.empty()) h->chunk_cost.assign((size_t)h->d.max_frames + 1, -1.0);
+  double& c = h->chunk_cost[F];
+  if (c < 0.0) {
+    h->planning = true;
+    h->plan_cost = 0.0;
+    // any non-null frame pointer: the launchers choose their kernel by it and record the grid
+    const int rc = forward_chunk(h, (const float*)h->zero, F, nullptr, nullptr);
+    h->planning = false;
+    c = rc ? 1e300 : h->plan_cost;
   }
-  return h->chunk_cost[F];
+  return c;
 }
 
 static const std::vector<int>& plan_chunks(eosv_handle* h, int B) {

@@ -181,8 +181,9 @@ __global__ __launch_bounds__(MT) void match_cosine_kernel(const float* __restric
 // (d-chunks of SG_DK staged through LDS in order), stored f32; smoothed[s][g] =
 // fma(l1, d[s+1][g], fma(l2, d[s][g], l1 * d[s-1][g])) with zeros outside the row's episode;
 // per row the (value, column) minimum of the block's columns is merged into ids[s] by a 64-bit
-// atomic min on (float bits << 32 | g): the values are >= 0, so their bit patterns order like
-// the floats, and equal values resolve to the smaller g (np.argsort(...)[:, 0] on ties).
+// atomic min on (ordered float key << 32 | g): the key maps the float's bits to an unsigned
+// value that orders like the float for either sign (NaN after +inf, as argsort puts it), and
+// equal values resolve to the smaller g (np.argsort(...)[:, 0] on ties).
 constexpr int SG_G = 64, SG_S = 64, SG_DK = 32;
 constexpr int SG_R = SG_S + 2;             // computed rows (halo included)
 constexpr int SG_RPT = (SG_R + 3) / 4;     // rows per thread (4 row groups of 64 threads)
@@ -239,7 +240,11 @@ __global__ __launch_bounds__(256) void seg_match_kernel(const float* __restrict_
     const float dp = sl + 1 < S ? dl[lr + 1][gl] : 0.f;
     const float v = fmaf(l1, dp, fmaf(l2, dl[lr][gl], l1 * dm));
     if (out && g < G) out[(long long)row * G + g] = v;
-    unsigned long long key = g < G ? ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)g : ~0ull;
+    // order-preserving key of the float (negative values, e.g. from lamda1/lamda2 < 0 set in
+    // utils, flip all bits; the others get the sign bit), -0 folded into +0 as argsort ties them
+    const unsigned vb = __float_as_uint(v == 0.f ? 0.f : v);
+    const unsigned ob = (vb & 0x80000000u) ? ~vb : (vb | 0x80000000u);
+    unsigned long long key = g < G ? ((unsigned long long)ob << 32) | (unsigned)g : ~0ull;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const unsigned long long ok = __shfl_xor(key, o, 64);

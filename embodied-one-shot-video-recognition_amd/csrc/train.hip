@@ -499,6 +499,14 @@ __global__ void softmax_xent_kernel(const float* __restrict__ logits, const int*
   }
   se = red[0];
   const int lab = labels[b];
+  if ((unsigned)lab >= (unsigned)C) {
+    // nn.CrossEntropyLoss raises 'Target out of bounds'; the host checks first
+    // (NativeTrainer.step), and a label that gets here anyway yields a NaN loss and a zero
+    // gradient for its row instead of an out-of-bounds read
+    for (int c = threadIdx.x; c < C; c += blockDim.x) dlogits[(long long)b * C + c] = 0.f;
+    if (threadIdx.x == 0) row_loss[b] = __int_as_float(0x7fc00000);
+    return;
+  }
   for (int c = threadIdx.x; c < C; c += blockDim.x)
     dlogits[(long long)b * C + c] = (expf(l[c] - m) / se - (c == lab ? 1.f : 0.f)) / (float)B;
   if (threadIdx.x == 0) row_loss[b] = (logf(se) + m - l[lab]) / (float)B;

@@ -14,6 +14,24 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # profiling build with the A/B switches and ablations compiled in, `make -C csrc prof`)
 LIB_PATH = os.environ.get("EOSV_LIBRARY") or os.path.join(PKG_ROOT, "libeosv.so")
 
+def source_digest() -> str:
+    """sha256 (16 hex) of the library's sources (csrc/*.hip, common.h, include/eosv.h): ties a
+    profile (e.g. profiles/*_traffic.json) to the kernels it measured; computable on the GPU box,
+    where there is no git history."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    repo = os.path.dirname(PKG_ROOT)
+    files = sorted(glob.glob(os.path.join(PKG_ROOT, "csrc", "*.hip"))) + \
+        [os.path.join(PKG_ROOT, "csrc", "common.h"), os.path.join(repo, "include", "eosv.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 EOSV_F32, EOSV_BF16, EOSV_F32X3 = 0, 1, 2
 MATCH_PROTONET, MATCH_COSINE = 0, 1
 MAX_COLS = 64

@@ -102,6 +102,26 @@ def sum_over_ranks(x: int) -> int:
     return int(t.item())
 
 
+def gather_values(x: float):
+    """[x of rank 0, x of rank 1, ...] on every rank (one all-gather of an f64 scalar)."""
+    d, _, n_ranks = world()
+    if d is None:
+        return [float(x)]
+    dev = _coll_device(d)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(n_ranks)]
+    d.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
+def describe():
+    """What the process group itself reports: backend name and world size (None when single-process)."""
+    d, _, _ = world()
+    if d is None:
+        return {"backend": None, "world_size_reported_by_backend": 1}
+    return {"backend": d.get_backend(), "world_size_reported_by_backend": d.get_world_size()}
+
+
 def episode_accs(preds: np.ndarray, query_y: Sequence[int]):
     """np.mean(query_y == predicted_y) per episode (network_test.py:159): 0.0 / 1.0."""
     return [np.mean(np.array([query_y[e]], np.float32) == preds[e]) for e in range(len(preds))]

@@ -291,9 +291,15 @@ class NativeTrainer:
         if NT % T:
             raise ValueError("frames must be B*T clip-major rows")
         B = NT // T
-        lab = torch.as_tensor(np.asarray(labels, np.int32).reshape(-1), device=self.dev)
-        if lab.numel() != B:
+        lab_h = np.asarray(labels).reshape(-1).astype(np.int64)
+        if lab_h.size != B:
             raise ValueError("one label per clip")
+        C = int(self.fc_w.shape[0])
+        if lab_h.size and (lab_h.min() < 0 or lab_h.max() >= C):
+            # nn.CrossEntropyLoss (network_train.py:85) raises on such a target
+            raise ValueError(f"NativeTrainer.step: label out of range [0, {C}): "
+                             f"min {int(lab_h.min())}, max {int(lab_h.max())} (num_classes too small for the list?)")
+        lab = torch.as_tensor(lab_h.astype(np.int32), device=self.dev)
         s = stream_ptr()
         L = self.L
         # ---- forward

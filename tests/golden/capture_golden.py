@@ -331,7 +331,9 @@ def capture_aug(mods, seed, episodes, tag, compact=False):
                         query_feature=np.stack([p["query_feature"] for p in rec.predicts]),
                         pred=np.stack([p["pred"] for p in rec.predicts]).astype(np.int64),
                         distance_row0=np.stack([q["distance"][0] for q in pool]),
-                        smoothed=np.stack([q["smoothed"] for q in pool]).astype(np.float32))
+                        smoothed=np.stack([q["smoothed"] for q in pool]).astype(np.float32),
+                        dists=(dists := np.stack([_proto_dists(p) for p in rec.predicts])),
+                        margin=(lambda s_: (s_[:, 1] - s_[:, 0]) / s_[:, 0])(np.sort(dists, axis=1)))
     if compact:
         compact_aug(os.path.join(OUT, f"{tag}.npz"))
     with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
@@ -441,7 +443,9 @@ def capture_shaped(mods, arch_name, kind, seed, episodes, tag, n_way, k_shot, T,
                             margin=(srt[:, 1] - srt[:, 0]) / srt[:, 0], proj=proj, proj_vector_seed=20261016)
         meta["acc_file_sha256"] = hashlib.sha256(acc_text.encode()).hexdigest()
         meta["acc_file_tail"] = acc_text.splitlines()[-1]
-        pin_plans_to_fixture(meta)
+        meta["near_ties"] = int(((srt[:, 1] - srt[:, 0]) / srt[:, 0] < 1e-5).sum())
+        if seed == 0:
+            pin_plans_to_fixture(meta)
     with open(os.path.join(OUT, f"{tag}.json"), "w") as f:
         json.dump(meta, f, indent=None if not features else 1)
     print(tag, "acc", acc_text.strip().splitlines()[-1])
@@ -613,6 +617,38 @@ def capture_train(mods, arch_name, tag, T=8, res=96, batch=2, epochs=2, step_siz
     print(tag, "losses", [round(l, 6) for l in losses])
 
 
+def make_long_list(src, path, T):
+    """The reference's test list without the videos shorter than T frames: at 256x256 the
+    reference cannot run an episode holding one (its zero padding is hard-coded 224x224,
+    utils.py:252, and torch.stack fails), so the wide config-5 fixtures sample from this list."""
+    keep = [l.strip() for l in open(src) if l.strip() and synth.frame_count(l.strip()) >= T]
+    with open(path, "w") as f:
+        f.write("\n".join(keep) + "\n")
+    return len(keep)
+
+
+def capture_wide(mods, only=None):
+    """Round-3 wide fixtures at every BASELINE episode shape, compact form (per-episode f64
+    prototype distances, top-2 margins, embedding projections, the result file's sha256):
+    config 4 30 episodes, config 5 10 (R50) + 5 (R101) episodes, config 3 30 episodes."""
+    jobs = {
+        "c4": lambda: capture_shaped(mods, "resnet50", "protonet", seed=8, episodes=30,
+                                     tag="c4_r50_14w1s_t32_seed8_wide", n_way=14, k_shot=1, T=32,
+                                     test_list="unreal14.list", features=False),
+        "c5r50": lambda: capture_shaped(mods, "resnet50", "protonet", seed=40, episodes=10,
+                                        tag="c5_r50_5w5s_t64_256_seed40_wide", n_way=5, k_shot=5, T=64, res=256,
+                                        test_list="test_long64.list", features=False),
+        "c5r101": lambda: capture_shaped(mods, "resnet50", "protonet", seed=41, episodes=5,
+                                         tag="c5_r101_5w5s_t64_256_seed41_wide", n_way=5, k_shot=5, T=64, res=256,
+                                         test_list="test_long64.list", backbone="resnet101", features=False),
+        "c3": lambda: capture_aug(mods, seed=9, episodes=30, tag="c3_r50_aug_seed9_wide", compact=True),
+    }
+    make_long_list(os.path.join(REF, "sources/data/test.list"), os.path.join(OUT, "test_long64.list"), 64)
+    for k, f in jobs.items():
+        if only is None or k in only:
+            f()
+
+
 def make_unreal14_list(path):
     """An UnrealAction-shaped novel split (README.md:23-26: 14 actions, 10 real target videos
     each), in the reference's ``class/video`` list format; names are synthetic."""
@@ -632,13 +668,19 @@ def main():
     ap.add_argument("--svm", action="store_true", help="only the SVM-classifier baseline episodes")
     ap.add_argument("--aug-seed6", action="store_true", help="only the 8-episode config-3 fixture")
     ap.add_argument("--train", action="store_true", help="only the training-loop fixtures (R18, R50)")
+    ap.add_argument("--wide", default=None,
+                    help="only the round-3 wide fixtures: comma-separated subset of c4,c5r50,c5r101,c3 (or 'all')")
+    ap.add_argument("--threads", type=int, default=8)
     args = ap.parse_args()
-    torch.set_num_threads(8)
+    torch.set_num_threads(args.threads)
     _install_stubs()
     gallery_path = os.path.join(tempfile.mkdtemp(), "gallery.list")
     mods = _import_reference(gallery_path)
     if args.layers:
         capture_layer_checksums(mods, "layers_one_frame")
+        return
+    if args.wide:
+        capture_wide(mods, None if args.wide == "all" else args.wide.split(","))
         return
     if args.train:
         capture_train(mods, "resnet18", "train_r18_t8_96")

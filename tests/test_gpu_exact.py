@@ -68,6 +68,22 @@ def test_segment_match_bit_exact(E, S, G, D):
         assert np.array_equal(ids[e * S:(e + 1) * S], np.argsort(ref, axis=1)[:, 0])
 
 
+@pytest.mark.parametrize("l1,l2", [(0.1, -1.0), (-0.6, 1.0)])
+def test_segment_match_negative_lambdas(l1, l2):
+    """utils.lamda1 / lamda2 are read at call time, so a user may set them negative: smoothed
+    distances then go negative (all, or some of them) and the argmin must still be argsort's."""
+    rng = np.random.default_rng(int(l1 * 10) + 50)
+    S, G, D = 40, 700, 64
+    seg = rng.random((S, D), dtype=np.float32)
+    gal = rng.random((G, D), dtype=np.float32)
+    ids, dist = engine.segment_match_episodes(torch.from_numpy(seg).cuda(), 1, torch.from_numpy(gal).cuda(), l1, l2,
+                                              with_dist=True)
+    ref = harness_ref.temporal_smooth(cdist(seg, gal, "euclidean"), l1, l2)
+    assert (ref < 0).any()
+    assert np.array_equal(dist.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(ids.cpu().numpy(), np.argsort(ref, axis=1)[:, 0])
+
+
 def test_segment_match_ties_pick_first_column():
     """Identical gallery rows: equal smoothed values, the first column wins (argsort[:, 0])."""
     rng = np.random.default_rng(9)

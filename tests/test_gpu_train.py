@@ -109,6 +109,35 @@ def test_train_kernels_reject_bad_arguments():
               "eosv_bn_train_forward")
 
 
+def test_train_rejects_out_of_range_labels():
+    """nn.CrossEntropyLoss (network_train.py:85) raises 'Target out of bounds' for a label outside
+    [0, num_classes): NativeTrainer.step raises before launching, and the kernel itself, given such a
+    label through the C ABI, returns a NaN loss and a zero gradient row (no out-of-bounds read)."""
+    from eosv._lib import check, lib, stream_ptr
+
+    tr = NativeTrainer("resnet18", 5, device=0)
+    tr.load_state_dict(synth.synth_state_dict(arch.SPECS["resnet18"], 5, 0))
+    frames = torch.randn(2 * 2, 3, 64, 64, device="cuda")
+    for bad in ([0, 5], [-1, 0]):
+        with pytest.raises(ValueError, match="label out of range"):
+            tr.step(frames, bad, 2, 1e-3, 1e-2)
+    L = lib()
+    B, C = 3, 5
+    logits = torch.randn(B, C, device="cuda")
+    lab = torch.tensor([1, 7, 4], dtype=torch.int32, device="cuda")
+    row_loss = torch.empty(B, device="cuda")
+    dlog = torch.full((B, C), 9.0, device="cuda")
+    check(L.eosv_softmax_xent(logits.data_ptr(), lab.data_ptr(), B, C, row_loss.data_ptr(), dlog.data_ptr(),
+                              stream_ptr()), "eosv_softmax_xent")
+    torch.cuda.synchronize()
+    assert torch.isnan(row_loss[1]) and torch.isfinite(row_loss[[0, 2]]).all()
+    assert (dlog[1] == 0).all()
+    ref = torch.softmax(logits[[0, 2]], 1)
+    ref[0, 1] -= 1
+    ref[1, 4] -= 1
+    assert torch.allclose(dlog[[0, 2]], ref / B, atol=1e-6)
+
+
 def _call(fn, *args):
     from eosv._lib import check, stream_ptr
 

@@ -116,5 +116,10 @@ if bench:  # the workload these counters belong to (bench.py attaches them only 
     mm = re.search(r"(resnet\d+), (\d+)x(\d+)", bench["config"]["workload"])
     if mm:
         traffic["key"] = f"{mm.group(1)}@{mm.group(2)}x{mm.group(3)}"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "embodied-one-shot-video-recognition_amd"))
+from eosv._lib import source_digest  # noqa: E402
+
+traffic["src_sha16"] = source_digest()  # bench.py attaches these counters only to the same kernels
 open(f"{dst}/{tag}_traffic.json", "w").write(json.dumps(traffic, indent=1) + "\n")
 print("\n".join(out))
