@@ -150,12 +150,17 @@ struct Pair1x1Args {
   const float* b1;   // [c1]
   void* y;           // [M][256]  conv3 output (the next block's residual)
   void* z;           // [M][c1]   next conv1 output
-  long long M;       // pixels, a multiple of 64
+  long long M;       // pixels, a multiple of 64 (pair1x1); any (pairw)
   int c1, cds;
   LaunchInfo* plan;  // non-null: record the grid only
+  int cmid, cexp;    // pairw_bf16: conv3 is 1x1 cmid -> cexp, the next conv1 cexp -> c1
 };
 bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
+// pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
+// streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
+bool pairw_bf16_ok(int cmid, int cexp, int c1, long long M);
+int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv

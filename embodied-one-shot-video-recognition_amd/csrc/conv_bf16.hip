@@ -31,6 +31,30 @@ __device__ __forceinline__ u16 f_to_bf(float f) { return __bfloat16_as_ushort(__
 // cycles per FLOP, but the chip holds a higher clock on it with random operands)
 // SPLIT: EOSV_F32X3 (ConvArgs::split): A reads virtual channel blocks (hi, lo, hi) of the stored
 // (hi, lo) pixels; epilogue residual = hi + lo, output stored as (hi, lo)
+// Tap order of a stride-2 3x3 conv's K loop (r03).  Its taps fall into four classes by the
+// parity of (kh, kw): (0|2, 0|2), (0|2, 1), (1, 0|2), (1, 1) read disjoint input pixels, and
+// the taps of one class read (nearly) the same pixels: kh = 0 and 2 are one input row apart,
+// i.e. the next output row's kh = 0.  K-steps walk the taps class by class, so a pixel line's
+// re-reads come one K-step apart and hit L2 (in (kh, kw) order they came 2-3 K-steps apart,
+// when 32 CUs' staging had turned the XCD's L2 over: L2 hit rate 0.32-0.41, PMC r03).  Weights
+// and pixels are indexed by the same tap, so only the accumulation order changes.
+__device__ __forceinline__ int tap_order(const ConvArgs& a, int t) {
+  constexpr unsigned long long PERM9 = 0x453718620ull;  // t -> tap: 0 2 6 8 1 7 3 5 4
+  return (a.stride == 2 && a.KH == 3 && a.KW == 3) ? (int)((PERM9 >> (4 * t)) & 15) : t;
+}
+// weight column (the stored K order) of the K-step starting at k0 of the kernel's K loop
+__device__ __forceinline__ int wcol(const ConvArgs& a, int k0) {
+  if (a.x2 && k0 >= a.K1) return k0;  // folded downsample columns
+  const int taps = a.KH * a.KW;
+  if (taps == 1) return k0;
+  if (a.kcm) {
+    const int chunk = k0 / (64 * taps);
+    return chunk * 64 * taps + tap_order(a, (k0 - chunk * 64 * taps) >> 6) * 64;
+  }
+  const int t = k0 / a.Cin;
+  return tap_order(a, t) * a.Cin + (k0 - t * a.Cin);
+}
+
 template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int BK = 64;  // bf16 elements per row = 128 B
@@ -128,14 +152,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
       }
     } else {
       int tap, c0;
+      const int taps = a.KH * a.KW;
       if (a.kcm) {  // K = (cin / 64, kh, kw, cin % 64)
-        const int taps = a.KH * a.KW;
         const int chunk = k0 / (64 * taps);
-        tap = (k0 - chunk * 64 * taps) >> 6;
+        tap = tap_order(a, (k0 - chunk * 64 * taps) >> 6);
         c0 = chunk * 64;
       } else {
         tap = k0 / a.Cin;
         c0 = k0 - tap * a.Cin;
+        tap = tap_order(a, tap);
       }
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
@@ -150,9 +175,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
       }
     }
     if (skip & 8) return;
+    const int kb = STEM ? k0 : wcol(a, k0);
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
-      const u16* src = brow[j] ? brow[j] + k0 : zero;
+      const u16* src = brow[j] ? brow[j] + kb : zero;
       u16* dst = Bs + (wid * (BN / NW) + 8 * j) * BK;
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }

@@ -482,11 +482,18 @@ static bool pair_enabled() {
   return v;
 }
 
+// ... and in the wider stages 2-3 (pairw_bf16.hip).  EOSV_PAIRW=0 (profiling build): unfused there.
+static bool pairw_enabled() {
+  static const bool v = env_switch("EOSV_PAIRW", 1) != 0;
+  return v;
+}
+
 static bool pair_ok(const eosv_handle* h, const Block& b, const Block* nb, long long M) {
   if (!pair_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || !nb || !nb->bottleneck) return false;
   const Conv &c3 = b.c3, &n1 = nb->c1;
   if (b.c2.stride != 1 || c3.kh != 1 || n1.kh != 1 || n1.stride != 1 || n1.cin != c3.cout) return false;
   if (b.has_ds && !(b.fuse_ds && b.ds.stride == 1)) return false;
+  if (c3.cin != 64) return pairw_enabled() && !b.has_ds && pairw_bf16_ok(c3.cin, c3.cout, n1.cout, M);
   return pair1x1_bf16_ok(c3.cin, c3.cout, n1.cout, b.has_ds ? c3.kds : 0, M);
 }
 
@@ -507,11 +514,14 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
   p.M = M;
   p.c1 = nb.c1.cout;
   p.cds = x2 ? b.c3.kds : 0;
+  p.cmid = b.c3.cin;
+  p.cexp = b.c3.cout;
+  const bool wide = p.cmid != 64;
   const double flops = 2.0 * M * ((double)b.c3.cout * (b.c3.cin + p.cds) + (double)nb.c1.cout * nb.c1.cin);
   if (h->planning) {
     LaunchInfo li{};
     p.plan = &li;
-    const int prc = launch_pair1x1_bf16(p, s);
+    const int prc = wide ? launch_pairw_bf16(p, s) : launch_pair1x1_bf16(p, s);
     if (prc == EOSV_OK) add_plan_cost(h, li, flops);
     return prc;
   }
@@ -522,7 +532,7 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
     if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
     EOSV_HIP_CHECK(hipEventRecord(e0, s));
   }
-  const int rc = launch_pair1x1_bf16(p, s);
+  const int rc = wide ? launch_pairw_bf16(p, s) : launch_pair1x1_bf16(p, s);
   if (h->prof && rc == EOSV_OK) {
     EOSV_HIP_CHECK(hipEventRecord(e1, s));
     h->recs.push_back({b.c3.id, e0, e1, flops});

@@ -1,0 +1,305 @@
+// Fused 1x1 pair for the bf16 bottleneck stages 2-3 (ResNet-50/101 layer2 / layer3): block b's
+// conv3 (1x1 CMID -> CEXP, folded BN, + residual, ReLU) and block b+1's conv1 (1x1 CEXP -> C1,
+// folded BN, ReLU) in one pass over the pixels (torchvision Bottleneck.forward: conv3 -> bn3 ->
+// += identity -> relu, then the next block's conv1 -> bn1 -> relu; reference models.py:19 via
+// self.convnet, driven from network_test.py:59).
+//
+// Unfused, the CEXP-channel map Y that conv3 writes is read straight back by the next conv1.
+// Both 1x1s are HBM-bound (conv3 at 57-114 FLOP/B, conv1 at 102-205 FLOP/B against the bf16
+// ridge of 315), so the pair's floor is its bytes: per pixel X (CMID) + R (CEXP) -> Y (CEXP) +
+// Z (C1), without the second read of Y (stage 2: 2.5 KB instead of 3.5 KB per pixel).
+//
+// The stage-1 pair (pair1x1_bf16.hip) keeps both weight matrices in LDS; here they are 128 KB
+// to 512 KB each, so they stream through LDS instead and Y never leaves registers:
+//   * persistent workgroups of 8 waves (one per CU); a round is 128 pixels, 16 per wave;
+//   * the CEXP channels go in chunks of 64: a 2-slot LDS ring holds a chunk's W3 rows
+//     (64 x CMID) and W1 columns (C1 x 64), filled by LDS-DMA one chunk ahead, one barrier per
+//     chunk; every wave reads the same slot for its own 16 pixels;
+//   * GEMM1 per chunk: D1[64 cout][16 px] = W3c . X^T on v_mfma_f32_16x16x32_bf16, the X
+//     fragments of the wave's pixels held in registers for the whole round; W3 rows are permuted
+//     (MFMA tile i, row 4q + e holds cout 32(i >> 1) + 8q + 4(i & 1) + e, as in pair1x1_bf16) so
+//     a lane ends up with couts 8q .. 8q + 7 and 32 + 8q .. 32 + 8q + 7 of pixel r: 16-B residual
+//     loads and Y stores, and after bias + residual + ReLU + bf16 exactly the B fragments of the
+//     chunk's two 32-wide k-slices of GEMM2;
+//   * GEMM2 accumulates D2[C1][16 px] += W1c . Ychunk^T chunk by chunk, then bias + ReLU -> Z.
+// K is walked in the unfused kernels' order (32-wide slices, increasing k), bias then residual
+// then ReLU then round-to-nearest bf16: both maps equal the unfused conv3 -> conv1 pair's bit for
+// bit (tests/native/conv_check.cpp).  The residual of chunk ch + 1 is loaded while chunk ch
+// computes, the next round's X during the round's last chunk; loads / stores use buffer resources based at the round's first
+// pixel, so tail pixels (M % 128) read zeros and their stores are dropped, without a branch.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+
+namespace eosv {
+
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_t;
+
+__device__ __forceinline__ float lo_f(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ unsigned f2bf(float f) { return (unsigned)__bfloat16_as_ushort(__float2bfloat16(f)); }
+// MFMA tile i, row t (0..15) -> channel within the 64-channel group
+__device__ __forceinline__ int permrow(int i, int t) { return 32 * (i >> 1) + 8 * (t >> 2) + 4 * (i & 1) + (t & 3); }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes > 0x7fffffffLL ? 0x7fffffffLL : bytes),
+                                           0x00020000);
+}
+// one 1-KiB LDS-DMA piece (a free function: the builtin inside a lambda drops the kernel's host stub)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 0);
+}
+}  // namespace
+
+constexpr int PW_WAVES = 8, PW_PX = 16, PW_TILE = PW_WAVES * PW_PX;
+
+template <int CMID, int CEXP, int C1>
+struct PairW {
+  static constexpr int W3B = 64 * CMID * 2;  // a chunk's W3 rows (64 couts x CMID), bytes
+  static constexpr int W1B = C1 * 64 * 2;    // a chunk's W1 columns (C1 x 64 k), bytes
+  static constexpr int STAGE = W3B + W1B;
+  static constexpr int PPW = STAGE / 1024 / PW_WAVES;  // 1-KiB DMA pieces per wave per chunk
+  static constexpr int NCH = CEXP / 64;
+  static constexpr int XS = CMID / 32;  // X fragments (k-slices of GEMM1) per lane
+  static constexpr int G2 = C1 / 64;    // 64-cout groups of GEMM2
+  static constexpr int LDS = 2 * STAGE + (CEXP + C1) * 4;
+  static_assert(STAGE % (1024 * PW_WAVES) == 0 && W3B % 1024 == 0, "DMA pieces");
+  static_assert(NCH % 2 == 0, "ring slots / residual ring");
+};
+
+template <int CMID, int CEXP, int C1>
+__global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
+  using P = PairW<CMID, CEXP, C1>;
+  constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS];
+  float* const b3s = (float*)(smem + 2 * P::STAGE);
+  float* const b1s = b3s + CEXP;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const long long M = a.M;
+  const long long nrounds = (M + PW_TILE - 1) / PW_TILE;
+  long long rt = blockIdx.x;  // launch: gridDim.x <= nrounds
+
+  for (int i = tid; i < CEXP; i += 512) b3s[i] = a.b3[i];
+  for (int i = tid; i < C1; i += 512) b1s[i] = a.b1[i];
+
+  // ---- weight DMA: piece j of this wave covers stage bytes [o, o + 1024), lane 16 B of it.
+  // Per lane the source offset within a chunk is fixed (vrel); the chunk moves it by a scalar.
+  const __amdgpu_buffer_rsrc_t w3r = rsrc(a.w3, (long long)CEXP * CMID * 2);
+  const __amdgpu_buffer_rsrc_t w1r = rsrc(a.w1, (long long)C1 * CEXP * 2);
+  int vrel[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int o = (w * PPW + j) * 1024 + lane * 16;
+    if (o < P::W3B) {  // W3 row R (tile R >> 4, row R & 15), 16-B chunk c' = c ^ (R & 15)
+      const int R = o / (CMID * 2), cs = (o % (CMID * 2)) / 16;
+      const int c = cs ^ (R & 15);
+      vrel[j] = (permrow(R >> 4, R & 15) * CMID + 8 * c) * 2;
+    } else {  // W1 row RR (group RR >> 6, tile (RR >> 4) & 3, row RR & 15), c' = c ^ ((RR >> 1) & 7)
+      const int o1 = o - P::W3B;
+      const int RR = o1 / 128, cs = (o1 % 128) / 16;
+      const int c = cs ^ ((RR >> 1) & 7);
+      vrel[j] = ((64 * (RR >> 6) + permrow((RR >> 4) & 3, RR & 15)) * CEXP + 8 * c) * 2;
+    }
+  }
+  auto dma = [&](int ch, int slot) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int o = (w * PPW + j) * 1024;  // wave-uniform
+      unsigned char* dst = smem + slot * P::STAGE + o;
+      if (o < P::W3B)
+        dma16(w3r, dst, vrel[j], ch * 64 * CMID * 2);
+      else
+        dma16(w1r, dst, vrel[j], ch * 128);
+    }
+  };
+
+  // ---- per-round resources (based at the round's first pixel; tails read 0, stores dropped)
+  struct RoundRes {
+    __amdgpu_buffer_rsrc_t x, res, y, z;
+  };
+  auto round_res = [&](long long t) {
+    RoundRes rr;
+    const long long p0 = t * PW_TILE;
+    const long long n = t < nrounds ? (M - p0 < PW_TILE ? M - p0 : PW_TILE) : 0;
+    rr.x = rsrc((const unsigned short*)a.x + p0 * CMID, n * CMID * 2);
+    rr.res = rsrc((const unsigned short*)a.res + p0 * CEXP, n * CEXP * 2);
+    rr.y = rsrc((unsigned short*)a.y + p0 * CEXP, n * CEXP * 2);
+    rr.z = rsrc((unsigned short*)a.z + p0 * C1, n * C1 * 2);
+    return rr;
+  };
+  const int pr = PW_PX * w + r;  // the lane's pixel within a round
+  auto load_x = [&](const RoundRes& rr, v4u* xf) {
+#pragma unroll
+    for (int s = 0; s < XS; ++s) xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rr.x, (pr * CMID + 32 * s + 8 * q) * 2, 0, 0);
+  };
+  auto load_r = [&](const RoundRes& rr, int ch, v4u* rv) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      rv[hh] = __builtin_amdgcn_raw_buffer_load_b128(rr.res, (pr * CEXP + ch * 64 + 32 * hh + 8 * q) * 2, 0, 0);
+  };
+
+  RoundRes cur = round_res(rt);
+  v4u xf[XS], rres[2][2];
+  dma(0, 0);
+  load_x(cur, xf);
+  load_r(cur, 0, rres[0]);
+
+  for (; rt < nrounds; rt += gridDim.x) {
+    const RoundRes nxt = round_res(rt + gridDim.x);
+    f32x4 acc2[G2][4];
+#pragma unroll
+    for (int g = 0; g < G2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc2[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // chunk pairs: the ring slot and the residual register set are compile-time per half
+#pragma unroll 1
+    for (int cp = 0; cp < NCH; cp += 2)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ch = cp + u;
+      const int slot = u;
+      // this wave's DMA of chunk ch is done, then every wave's (barrier): the slot is complete,
+      // and slot ^ 1 (chunk ch - 1) is free for the next chunk's DMA.
+      // VMEM ops a wave issues after its DMA of chunk ch (in chunk ch - 1, order pinned by the
+      // sched_barriers): 2 residual loads and 2 Y stores, in the round's last chunk also the next
+      // round's XS X loads and 2 G2 Z stores; before the loop: XS X loads + 2 residual loads
+      if (u == 0 && cp == 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(XS + 2) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      dma(ch + 1 < NCH ? ch + 1 : 0, slot ^ 1);  // the last chunk prefetches the next round's chunk 0
+      if (u == 0 || cp + 2 < NCH)
+        load_r(cur, ch + 1, rres[u ^ 1]);
+      else
+        load_r(nxt, 0, rres[0]);
+      __builtin_amdgcn_sched_barrier(0);
+
+      const unsigned char* ws = smem + slot * P::STAGE;
+      // The chunk's A fragments come in NG groups of 4 (GEMM1 slices s = 0 .. XS - 1: W3 tiles
+      // i = 0..3; then GEMM2 (k-slice s2, cout group g): W1 tiles i = 0..3), software-pipelined:
+      // group gi + 1 is read from LDS while group gi's MFMAs run (sched_barriers keep the order and
+      // two groups of fragments live at most: two waves per SIMD, <= 256 VGPRs).
+      const unsigned char* w1s = ws + P::W3B;
+      constexpr int NG = XS + 2 * G2;
+      auto frags = [&](int gi, bf16x8* f) {
+        if (gi < XS) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) f[i] = *(const bf16x8*)(ws + (16 * i + r) * (CMID * 2) + (((4 * gi + q) ^ r) << 4));
+        } else {
+          const int s2 = (gi - XS) / G2, g = (gi - XS) % G2;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int RR = 64 * g + 16 * i + r;
+            f[i] = *(const bf16x8*)(w1s + RR * 128 + (((4 * s2 + q) ^ ((RR >> 1) & 7)) << 4));
+          }
+        }
+      };
+      bf16x8 fr[2][4];
+      frags(0, fr[0]);
+      f32x4 acc1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 yf[2];
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) {
+        if (gi + 1 < NG) frags(gi + 1, fr[(gi + 1) & 1]);
+        // the next group's 4 LDS reads issue before this group's 4 MFMAs
+        if (gi + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        if (gi < XS) {  // GEMM1: chunk couts, tiles i = 0..3 of 16 permuted rows
+          const bf16x8 bx = __builtin_bit_cast(bf16x8, xf[gi]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], bx, acc1[i], 0, 0, 0);
+        } else {  // GEMM2: D2[64g + permuted rows][px] += W1[.., k-slice s2 of the chunk] . Ychunk
+          const int s2 = (gi - XS) / G2, g = (gi - XS) % G2;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc2[g][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], yf[s2], acc2[g][i], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (gi == XS - 1) {
+          if (u == 1 && cp + 2 == NCH) {  // the round's X is dead: the next round's goes into the same registers
+            load_x(nxt, xf);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          // epilogue 1: + shift, + residual, ReLU, bf16 -> Y (global) and the GEMM2 B fragments
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int c0 = ch * 64 + 32 * hh + 8 * q;
+            const float4 bA = *(const float4*)(b3s + c0), bB = *(const float4*)(b3s + c0 + 4);
+            const float bb[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
+            const v4u rv = rres[u][hh];
+            v4u pk;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int e0 = 2 * k, e1 = 2 * k + 1;  // elements of the lane's 8 couts
+              float v0 = acc1[2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
+              float v1 = acc1[2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
+              v0 += lo_f(rv[k]);
+              v1 += hi_f(rv[k]);
+              pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, (pr * CEXP + c0) * 2, 0, 0);
+            yf[hh] = __builtin_bit_cast(bf16x8, pk);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // epilogue 2: + shift, ReLU, bf16 -> Z
+#pragma unroll
+    for (int g = 0; g < G2; ++g)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int c0 = 64 * g + 32 * hh + 8 * q;
+        v4u pk;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e0 = 2 * k, e1 = 2 * k + 1;
+          const float v0 = acc2[g][2 * hh + (e0 >> 2)][e0 & 3] + b1s[c0 + e0];
+          const float v1 = acc2[g][2 * hh + (e1 >> 2)][e1 & 3] + b1s[c0 + e1];
+          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, (pr * C1 + c0) * 2, 0, 0);
+      }
+    cur = nxt;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) chunk-0 prefetch has landed
+}
+
+template <int CMID, int CEXP, int C1>
+static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
+  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1>, 512);
+  const long long nrounds = (a.M + PW_TILE - 1) / PW_TILE;
+  if (a.plan) return record_launch(a.plan, nrounds, occ);
+  const long long grid = std::min<long long>(nrounds, (long long)occ * device_cu_count());
+  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1>), dim3((unsigned)grid), dim3(512), 0, s, a);
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
+bool pairw_bf16_ok(int cmid, int cexp, int c1, long long M) {
+  if (M <= 0) return false;
+  return (cmid == 128 && cexp == 512 && (c1 == 128 || c1 == 256)) || (cmid == 256 && cexp == 1024 && c1 == 256);
+}
+
+int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
+  if (!pairw_bf16_ok(a.cmid, a.cexp, a.c1, a.M) || a.x2 || a.cds || !a.x || !a.res || !a.w3 || !a.b3 || !a.w1 ||
+      !a.b1 || !a.y || !a.z)
+    return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
+  if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128>(a, s);
+  if (a.cmid == 128) return launch_pairw<128, 512, 256>(a, s);
+  return launch_pairw<256, 1024, 256>(a, s);
+}
+
+}  // namespace eosv

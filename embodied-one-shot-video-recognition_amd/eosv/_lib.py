@@ -73,7 +73,8 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise EosvError(f"{LIB_PATH} not built: run `make -C csrc` or __graft_entry__.build()")
-    L = ctypes.CDLL(LIB_PATH)
+    # RTLD_NOW: an unresolved symbol (e.g. a kernel stub the host pass dropped) fails here, at load
+    L = ctypes.CDLL(LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
     vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
     sig = {
         "eosv_create": (i32, [ctypes.POINTER(EosvDesc), ctypes.POINTER(vp)]),

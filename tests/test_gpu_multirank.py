@@ -37,6 +37,11 @@ tag, out = sys.argv[3], sys.argv[4]
 import json
 meta = json.load(open(os.path.join(sys.argv[2], "tests", "golden", tag + ".json")))
 utils.EPISODE_NUMS["test"] = len(meta["episodes"])
+if "n_way" in meta:  # an episode shape set the way a reference user sets it: the utils globals
+    utils.n_way, utils.k_shot, utils.VIDEO_FRAMES = meta["n_way"], meta["k_shot"], meta["video_frames"]
+    utils.IMG_crop_size = (meta["H"], meta["W"])
+    if meta.get("test_list", "sources/data/test.list") != "sources/data/test.list":
+        utils.TEST_LIST = os.path.join(sys.argv[2], "tests", "golden", meta["test_list"])
 pkl = out + ".model.pkl"
 if dist.get_rank() == 0:
     sd = synth.synth_state_dict(arch.SPECS[meta["arch"]], 64, 0)
@@ -63,14 +68,26 @@ def _spawn(argv, world, port, env_extra=None, timeout=240):
     return outs
 
 
-@pytest.mark.parametrize("tag", ["c1_r18_protonet_seed1", "c1_r18_cosine_seed2"])
+C4_WIDE = "c4_r50_14w1s_t32_seed8_wide"
+
+
+@pytest.mark.parametrize("tag", ["c1_r18_protonet_seed1", "c1_r18_cosine_seed2", "c4_r50_14w1s_t32_seed7"]
+                         + ([C4_WIDE] if os.path.exists(os.path.join(REPO, "tests", "golden", C4_WIDE + ".json")) else []))
 def test_dropin_baseline_two_ranks_writes_reference_file(tag, tmp_path):
+    """Config 4's shape too (BASELINE configs[3]: 14-way 1-shot, 16 segments, R50 over the
+    UnrealAction-shaped split, episodes sharded over ranks with one all-gather of the predictions):
+    2 ranks write the reference's result file byte for byte (network_test.py:159-167)."""
     script = tmp_path / "dropin.py"
     script.write_text(_DROPIN)
     out = str(tmp_path / "acc.txt")
-    _spawn([sys.executable, str(script), PKG, REPO, tag, out], 2, 29611 + os.getpid() % 500)
+    _spawn([sys.executable, str(script), PKG, REPO, tag, out], 2, 29611 + os.getpid() % 500, timeout=300)
     meta, _ = load_fixture(tag)
-    assert open(out).read() == meta["acc_file"]
+    text = open(out).read()
+    if "acc_file" in meta:
+        assert text == meta["acc_file"]
+    else:
+        import hashlib
+        assert hashlib.sha256(text.encode()).hexdigest() == meta["acc_file_sha256"]
 
 
 _DROPIN_AUG = r"""
@@ -152,3 +169,11 @@ def test_bench_spawns_ranks_and_matches_one_rank():
     # same 24 timed episodes (plans are drawn once in the reference's order and dealt e % world)
     assert two["episode_acc"] == one["episode_acc"]
     assert abs(two["value_per_gpu"] * 2 - two["value"]) < 0.02 * two["value"]
+    # the self-verifying record: what the process group reports, and every rank's share
+    d2, d1 = two["dist"], one["dist"]
+    assert d2["backend"] == "gloo" and d2["world_size_reported_by_backend"] == 2 and d2["launched_world_size"] == 2
+    assert d1["backend"] is None and d1["world_size_reported_by_backend"] == 1
+    assert len(d2["per_rank_clips"]) == 2 and len(d2["per_rank_elapsed_s"]) == 2
+    assert sum(d2["per_rank_clips"]) == sum(d1["per_rank_clips"]) == 24 * 6
+    clips = sum(d2["per_rank_clips"])
+    assert abs(two["value"] - clips / max(d2["per_rank_elapsed_s"])) <= 0.01 * two["value"]

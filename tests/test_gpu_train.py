@@ -18,6 +18,8 @@ max(4 x torch-f32's distance, 2e-2 relative) of f64 (a wrong kernel is off by O(
 parameter / BN running statistic after two steps within max(4 x torch-f32's distance, 1e-5
 relative), tensors compared by norm.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -61,6 +63,24 @@ def test_train_step_matches_torch_reference(name):
     T, B, H = 4, 2, 96
     frames = torch.randn(B * T, 3, H, H)
     labels = [3, 17]
+    _check_two_steps(name, frames, labels, T, H)
+
+
+@pytest.mark.timeout(600)
+def test_train_step_reference_shape_resnet50():
+    """The reference's own training shape (network_train.py:140,148: batch 6 clips x 16 frames at
+    224x224, ResNet-50): two NativeTrainer steps against the f64 replay, with the same f32
+    yardstick bounds as the small case (a batch of 96 frames conditions the backward far better,
+    so the yardstick is tighter here)."""
+    torch.manual_seed(1)
+    T, B, H = 16, 6, 224
+    frames = torch.randn(B * T, 3, H, H)
+    labels = [5, 0, 63, 17, 5, 40]
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    _check_two_steps("resnet50", frames, labels, T, H)
+
+
+def _check_two_steps(name, frames, labels, T, H):
     lr1, lr2 = 1e-3, 1e-2  # 10x the reference's (network_train.py:140)
     sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
     ref_losses, ref_g, ref_sd = _oracle(name, sd, frames, labels, T, lr1, lr2, 2, torch.float64)
@@ -71,7 +91,7 @@ def test_train_step_matches_torch_reference(name):
     l0, logits = tr.step(frames.cuda(), labels, T, lr1, lr2)
     g0 = tr.grads()
     l1, _ = tr.step(frames.cuda(), labels, T, lr1, lr2)
-    print(f"[{name}] loss {l0:.6f} / {ref_losses[0]:.6f}, {l1:.6f} / {ref_losses[1]:.6f}")
+    print(f"[{name} {tuple(frames.shape)}] loss {l0:.6f} / {ref_losses[0]:.6f}, {l1:.6f} / {ref_losses[1]:.6f}")
     assert abs(l0 - ref_losses[0]) <= 1e-4 * abs(ref_losses[0])
     # the second loss inherits the first step's gradient conditioning: same yardstick
     assert abs(l1 - ref_losses[1]) <= max(4 * abs(f32_losses[1] - ref_losses[1]), 1e-4 * abs(ref_losses[1]))
@@ -82,7 +102,7 @@ def test_train_step_matches_torch_reference(name):
         yard = float((f32_g[k] - gr).norm()) / norm
         worst = max(worst, err)
         assert err <= max(4 * yard, 2e-2), (k, err, yard)
-    print(f"[{name}] worst relative gradient error {worst:.2e}")
+    print(f"[{name} {tuple(frames.shape)}] worst relative gradient error {worst:.2e}")
     got = tr.state_dict()
     for k, v in ref_sd.items():
         if k.endswith("num_batches_tracked"):

@@ -30,6 +30,8 @@ for f in sys.argv[1:]:
             if "SQ_VALU_MFMA_BUSY_CYCLES" in v:
                 # MFMA busy cycles are summed over SIMDs: 256 CUs x 4 SIMDs
                 s += f" mfma_busy={v['SQ_VALU_MFMA_BUSY_CYCLES'] / (v['GRBM_GUI_ACTIVE'] / 8) / 1024:.2f}"
+        if "TCC_HIT_sum" in v and "TCC_MISS_sum" in v:
+            s += f" L2hit={v['TCC_HIT_sum'] / max(1.0, v['TCC_HIT_sum'] + v['TCC_MISS_sum']):.3f}"
         for c in sorted(v):
             if c not in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS",
                          "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"):
