@@ -24,9 +24,10 @@
 //   * GEMM2 accumulates D2[C1][16 px] += W1c . Ychunk^T chunk by chunk, then bias + ReLU -> Z.
 // K is walked in the unfused kernels' order (32-wide slices, increasing k), bias then residual
 // then ReLU then round-to-nearest bf16: both maps equal the unfused conv3 -> conv1 pair's bit for
-// bit (tests/native/conv_check.cpp).  The residual of chunk ch + 1 is loaded while chunk ch
+// bit (tests/native/conv_check.cpp).  The residual of chunk ch + 3 is loaded while chunk ch
 // computes, the next round's X during the round's last chunk; loads / stores use buffer resources based at the round's first
-// pixel, so tail pixels (M % 128) read zeros and their stores are dropped, without a branch.
+// pixel, so tail pixels (M % 128) read zeros and their stores are dropped, without a branch; their
+// per-lane part is the VGPR offset, the chunk / channel-group part the scalar offset.
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -48,35 +49,45 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long lo
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes > 0x7fffffffLL ? 0x7fffffffLL : bytes),
                                            0x00020000);
 }
-// one 1-KiB LDS-DMA piece (a free function: the builtin inside a lambda drops the kernel's host stub)
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 0);
+// one 1-KiB LDS-DMA piece (a free function: the builtin inside a lambda drops the kernel's host
+// stub).  global_load_lds, not buffer_load ... lds: after the buffer form hipcc waited vmcnt(0)
+// before the next LDS read (for every DMA in flight, the next chunk's included)
+__device__ __forceinline__ void dma16(const unsigned char* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_t*)lds, 16, 0, 0);
 }
 }  // namespace
 
-constexpr int PW_WAVES = 8, PW_PX = 16, PW_TILE = PW_WAVES * PW_PX;
+constexpr int PW_TILE = 128;  // pixels per round
 
-template <int CMID, int CEXP, int C1>
+// NPT: 16-pixel tiles per wave.  NPT = 1: 8 waves (two per SIMD); NPT = 2: 4 waves (one per SIMD,
+// 512 VGPRs) that read each LDS weight fragment once for 32 pixels -- the LDS feeds one fragment per
+// MFMA at NPT = 1, which at CMID 256 made the weight reads, not HBM, the pair's limit.
+template <int CMID, int CEXP, int C1, int NPT>
 struct PairW {
+  static constexpr int NW = 8 / NPT;                   // waves per workgroup
+  static constexpr int PX = 16 * NPT;                  // pixels per wave
   static constexpr int W3B = 64 * CMID * 2;  // a chunk's W3 rows (64 couts x CMID), bytes
   static constexpr int W1B = C1 * 64 * 2;    // a chunk's W1 columns (C1 x 64 k), bytes
-  static constexpr int STAGE = W3B + W1B;
-  static constexpr int PPW = STAGE / 1024 / PW_WAVES;  // 1-KiB DMA pieces per wave per chunk
+  static constexpr int STAGE_W = W3B + W1B;
+  // + the chunk's 64 conv3 BN shifts (256 B, DMA'd with the weights: an LDS read outside the ring
+  // slots made hipcc wait vmcnt(0), i.e. for the in-flight DMA, before it)
+  static constexpr int STAGE = STAGE_W + 256;
+  static constexpr int PPW = STAGE_W / 1024 / NW;  // 1-KiB DMA pieces per wave per chunk
   static constexpr int NCH = CEXP / 64;
   static constexpr int XS = CMID / 32;  // X fragments (k-slices of GEMM1) per lane
   static constexpr int G2 = C1 / 64;    // 64-cout groups of GEMM2
-  static constexpr int LDS = 2 * STAGE + (CEXP + C1) * 4;
-  static_assert(STAGE % (1024 * PW_WAVES) == 0 && W3B % 1024 == 0, "DMA pieces");
-  static_assert(NCH % 2 == 0, "ring slots / residual ring");
+  static constexpr int LDS = 2 * STAGE + C1 * 4;
+  static_assert(STAGE_W % (1024 * NW) == 0 && W3B % 1024 == 0 && PPW >= 2, "DMA pieces");
+  static_assert(NCH % 4 == 0, "ring slots / residual ring");
+  static_assert(PPW < XS + 2 * G2, "DMA pieces go out one per fragment group, the residual loads after them");
 };
 
-template <int CMID, int CEXP, int C1>
-__global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
-  using P = PairW<CMID, CEXP, C1>;
-  constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW;
+template <int CMID, int CEXP, int C1, int NPT>
+__global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a) {
+  using P = PairW<CMID, CEXP, C1, NPT>;
+  constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW, NT = 64 * P::NW;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS];
-  float* const b3s = (float*)(smem + 2 * P::STAGE);
-  float* const b1s = b3s + CEXP;
+  float* const b1s = (float*)(smem + 2 * P::STAGE);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -86,13 +97,12 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   const long long nrounds = (M + PW_TILE - 1) / PW_TILE;
   long long rt = blockIdx.x;  // launch: gridDim.x <= nrounds
 
-  for (int i = tid; i < CEXP; i += 512) b3s[i] = a.b3[i];
-  for (int i = tid; i < C1; i += 512) b1s[i] = a.b1[i];
+  for (int i = tid; i < C1; i += NT) b1s[i] = a.b1[i];
 
   // ---- weight DMA: piece j of this wave covers stage bytes [o, o + 1024), lane 16 B of it.
   // Per lane the source offset within a chunk is fixed (vrel); the chunk moves it by a scalar.
-  const __amdgpu_buffer_rsrc_t w3r = rsrc(a.w3, (long long)CEXP * CMID * 2);
-  const __amdgpu_buffer_rsrc_t w1r = rsrc(a.w1, (long long)C1 * CEXP * 2);
+  const unsigned char* w3b = (const unsigned char*)a.w3;
+  const unsigned char* w1b = (const unsigned char*)a.w1;
   int vrel[PPW];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) {
@@ -108,16 +118,15 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
       vrel[j] = ((64 * (RR >> 6) + permrow((RR >> 4) & 3, RR & 15)) * CEXP + 8 * c) * 2;
     }
   }
-  auto dma = [&](int ch, int slot) {
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int o = (w * PPW + j) * 1024;  // wave-uniform
-      unsigned char* dst = smem + slot * P::STAGE + o;
-      if (o < P::W3B)
-        dma16(w3r, dst, vrel[j], ch * 64 * CMID * 2);
-      else
-        dma16(w1r, dst, vrel[j], ch * 128);
-    }
+  auto dma_piece = [&](int j, int ch, int slot) {
+    const int o = (w * PPW + j) * 1024;  // wave-uniform
+    unsigned char* dst = smem + slot * P::STAGE + o;
+    if (o < P::W3B)
+      dma16(w3b + (long long)ch * 64 * CMID * 2 + vrel[j], dst);
+    else
+      dma16(w1b + ch * 128 + vrel[j], dst);
+    if (j == 0 && w == 0 && lane < 16)  // the chunk's conv3 shifts: 16 lanes x 16 B
+      dma16((const unsigned char*)(a.b3 + ch * 64) + lane * 16, smem + slot * P::STAGE + P::STAGE_W);
   };
 
   // ---- per-round resources (based at the round's first pixel; tails read 0, stores dropped)
@@ -134,55 +143,71 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
     rr.z = rsrc((unsigned short*)a.z + p0 * C1, n * C1 * 2);
     return rr;
   };
-  const int pr = PW_PX * w + r;  // the lane's pixel within a round
-  auto load_x = [&](const RoundRes& rr, v4u* xf) {
+  // the lane's pixels within a round: 16 t + r of the wave's block, t < NPT
+  const int pw = P::PX * w + r;
+  auto load_x = [&](const RoundRes& rr, v4u (*xf)[XS]) {
 #pragma unroll
-    for (int s = 0; s < XS; ++s) xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rr.x, (pr * CMID + 32 * s + 8 * q) * 2, 0, 0);
+    for (int t = 0; t < NPT; ++t)
+#pragma unroll
+      for (int s = 0; s < XS; ++s)
+        xf[t][s] = __builtin_amdgcn_raw_buffer_load_b128(rr.x, ((pw + 16 * t) * CMID + 8 * q) * 2, 64 * s, 0);
   };
-  auto load_r = [&](const RoundRes& rr, int ch, v4u* rv) {
+  auto load_r = [&](const RoundRes& rr, int ch, v4u (*rv)[2]) {
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-      rv[hh] = __builtin_amdgcn_raw_buffer_load_b128(rr.res, (pr * CEXP + ch * 64 + 32 * hh + 8 * q) * 2, 0, 0);
+    for (int t = 0; t < NPT; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        rv[t][hh] = __builtin_amdgcn_raw_buffer_load_b128(rr.res, ((pw + 16 * t) * CEXP + 8 * q) * 2,
+                                                          (ch * 64 + 32 * hh) * 2, 0);
   };
 
+  // the residual of chunk ch is loaded RD chunks ahead (HBM latency under load is several chunks
+  // of this loop: with one chunk of lead the epilogue waited on it), into a ring of 4 register sets
+  constexpr int RD = XS >= 8 ? 2 : 3;  // (CMID 256: one set fewer keeps the wave within 256 VGPRs)
   RoundRes cur = round_res(rt);
-  v4u xf[XS], rres[2][2];
-  dma(0, 0);
+  v4u xf[NPT][XS], rres[4][NPT][2];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) dma_piece(j, 0, 0);
   load_x(cur, xf);
-  load_r(cur, 0, rres[0]);
+#pragma unroll
+  for (int c = 0; c < RD; ++c) load_r(cur, c, rres[c]);
 
   for (; rt < nrounds; rt += gridDim.x) {
     const RoundRes nxt = round_res(rt + gridDim.x);
-    f32x4 acc2[G2][4];
+    f32x4 acc2[NPT][G2][4];
 #pragma unroll
-    for (int g = 0; g < G2; ++g)
+    for (int t = 0; t < NPT; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc2[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int g = 0; g < G2; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc2[t][g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // chunk pairs: the ring slot and the residual register set are compile-time per half
+    // chunk quads: the ring slot and the residual register set are compile-time per step
 #pragma unroll 1
-    for (int cp = 0; cp < NCH; cp += 2)
+    for (int cp = 0; cp < NCH; cp += 4)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int ch = cp + u;
-      const int slot = u;
-      // this wave's DMA of chunk ch is done, then every wave's (barrier): the slot is complete,
-      // and slot ^ 1 (chunk ch - 1) is free for the next chunk's DMA.
-      // VMEM ops a wave issues after its DMA of chunk ch (in chunk ch - 1, order pinned by the
-      // sched_barriers): 2 residual loads and 2 Y stores, in the round's last chunk also the next
-      // round's XS X loads and 2 G2 Z stores; before the loop: XS X loads + 2 residual loads
-      if (u == 0 && cp == 0)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(XS + 2) : "memory");
+      const int slot = u & 1;
+      // This wave's DMA of chunk ch is done, then every wave's (barrier): the slot is complete,
+      // and slot ^ 1 (chunk ch - 1) is free for the next chunk's DMA.  In chunk ch - 1 the DMA
+      // pieces went out with its first PPW fragment groups (one per group: an LDS-DMA issue costs
+      // the wave ~60-185 cycles, so all of them at once idled the SIMD's MFMA pipe); the VMEM ops
+      // issued after the last piece (order pinned by the sched_barriers) may stay in flight:
+      // 2 NPT residual loads (group PPW), the 2 NPT Y stores and, in the round's last chunk, the
+      // next round's XS NPT X loads when the epilogue (after group XS - 1) follows the last piece,
+      // and the last chunk's 2 G2 NPT Z stores; before the loop: XS NPT X loads + 2 RD NPT residual
+      // loads after the pieces.
+      constexpr int YOUNG = 2 * NPT + (XS >= PPW ? 2 * NPT : 0);
+      constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0) + 2 * G2 * NPT;
+      constexpr int YOUNG_PRO = (XS + 2 * RD) * NPT;
+      if (u == 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST) : "memory");
       else
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YOUNG) : "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      dma(ch + 1 < NCH ? ch + 1 : 0, slot ^ 1);  // the last chunk prefetches the next round's chunk 0
-      if (u == 0 || cp + 2 < NCH)
-        load_r(cur, ch + 1, rres[u ^ 1]);
-      else
-        load_r(nxt, 0, rres[0]);
-      __builtin_amdgcn_sched_barrier(0);
+      const int nch = ch + 1 < NCH ? ch + 1 : 0;  // the last chunk prefetches the next round's chunk 0
 
       const unsigned char* ws = smem + slot * P::STAGE;
       // The chunk's A fragments come in NG groups of 4 (GEMM1 slices s = 0 .. XS - 1: W3 tiles
@@ -206,29 +231,45 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
       };
       bf16x8 fr[2][4];
       frags(0, fr[0]);
-      f32x4 acc1[4];
+      f32x4 acc1[NPT][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      bf16x8 yf[2];
+      for (int t = 0; t < NPT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc1[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 yf[NPT][2];
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
+        if (gi < PPW) dma_piece(gi, nch, slot ^ 1);
+        if (gi == PPW) {  // branch-free (scalar selects): a branch here made hipcc wait vmcnt(0) at the join
+          const bool here = ch + RD < NCH;
+          RoundRes rr;
+          rr.res = here ? cur.res : nxt.res;
+          load_r(rr, here ? ch + RD : ch + RD - NCH, rres[(u + RD) & 3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         if (gi + 1 < NG) frags(gi + 1, fr[(gi + 1) & 1]);
         // the next group's 4 LDS reads issue before this group's 4 MFMAs
         if (gi + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * NPT, 0);
         if (gi < XS) {  // GEMM1: chunk couts, tiles i = 0..3 of 16 permuted rows
-          const bf16x8 bx = __builtin_bit_cast(bf16x8, xf[gi]);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], bx, acc1[i], 0, 0, 0);
+          for (int t = 0; t < NPT; ++t) {
+            const bf16x8 bx = __builtin_bit_cast(bf16x8, xf[t][gi]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc1[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], bx, acc1[t][i], 0, 0, 0);
+          }
         } else {  // GEMM2: D2[64g + permuted rows][px] += W1[.., k-slice s2 of the chunk] . Ychunk
           const int s2 = (gi - XS) / G2, g = (gi - XS) % G2;
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc2[g][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], yf[s2], acc2[g][i], 0, 0, 0);
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc2[t][g][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], yf[t][s2], acc2[t][g][i], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (gi == XS - 1) {
-          if (u == 1 && cp + 2 == NCH) {  // the round's X is dead: the next round's goes into the same registers
+          if (u == 3 && cp + 4 == NCH) {  // the round's X is dead: the next round's goes into the same registers
             load_x(nxt, xf);
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -236,21 +277,29 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             const int c0 = ch * 64 + 32 * hh + 8 * q;
-            const float4 bA = *(const float4*)(b3s + c0), bB = *(const float4*)(b3s + c0 + 4);
-            const float bb[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
-            const v4u rv = rres[u][hh];
-            v4u pk;
+            // read as the fragments are (bf16x8 through the slot pointer): a float4 read here got a
+            // vmcnt(0) from hipcc, as if it could alias the DMA in flight
+            const unsigned char* b3c = ws + P::STAGE_W + (32 * hh + 8 * q) * 4;
+            const f32x4 bA = __builtin_bit_cast(f32x4, *(const bf16x8*)b3c);
+            const f32x4 bB = __builtin_bit_cast(f32x4, *(const bf16x8*)(b3c + 16));
+            const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int e0 = 2 * k, e1 = 2 * k + 1;  // elements of the lane's 8 couts
-              float v0 = acc1[2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-              float v1 = acc1[2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-              v0 += lo_f(rv[k]);
-              v1 += hi_f(rv[k]);
-              pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+            for (int t = 0; t < NPT; ++t) {
+              const v4u rv = rres[u][t][hh];  // ring slot ch & 3
+              v4u pk;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int e0 = 2 * k, e1 = 2 * k + 1;  // elements of the lane's 8 couts
+                float v0 = acc1[t][2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
+                float v1 = acc1[t][2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
+                v0 += lo_f(rv[k]);
+                v1 += hi_f(rv[k]);
+                pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+              }
+              __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2,
+                                                     (ch * 64 + 32 * hh) * 2, 0);
+              yf[t][hh] = __builtin_bit_cast(bf16x8, pk);
             }
-            __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, (pr * CEXP + c0) * 2, 0, 0);
-            yf[hh] = __builtin_bit_cast(bf16x8, pk);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -258,32 +307,34 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
     }
     // epilogue 2: + shift, ReLU, bf16 -> Z
 #pragma unroll
-    for (int g = 0; g < G2; ++g)
+    for (int t = 0; t < NPT; ++t)
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int c0 = 64 * g + 32 * hh + 8 * q;
-        v4u pk;
+      for (int g = 0; g < G2; ++g)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e0 = 2 * k, e1 = 2 * k + 1;
-          const float v0 = acc2[g][2 * hh + (e0 >> 2)][e0 & 3] + b1s[c0 + e0];
-          const float v1 = acc2[g][2 * hh + (e1 >> 2)][e1 & 3] + b1s[c0 + e1];
-          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+        for (int hh = 0; hh < 2; ++hh) {
+          const int c0 = 64 * g + 32 * hh + 8 * q;
+          v4u pk;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int e0 = 2 * k, e1 = 2 * k + 1;
+            const float v0 = acc2[t][g][2 * hh + (e0 >> 2)][e0 & 3] + b1s[c0 + e0];
+            const float v1 = acc2[t][g][2 * hh + (e1 >> 2)][e1 & 3] + b1s[c0 + e1];
+            pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, ((pw + 16 * t) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2, 0);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, (pr * C1 + c0) * 2, 0, 0);
-      }
     cur = nxt;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) chunk-0 prefetch has landed
 }
 
-template <int CMID, int CEXP, int C1>
+template <int CMID, int CEXP, int C1, int NPT>
 static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
-  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1>, 512);
+  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT>, 512 / NPT);
   const long long nrounds = (a.M + PW_TILE - 1) / PW_TILE;
   if (a.plan) return record_launch(a.plan, nrounds, occ);
   const long long grid = std::min<long long>(nrounds, (long long)occ * device_cu_count());
-  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1>), dim3((unsigned)grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -297,9 +348,9 @@ int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
   if (!pairw_bf16_ok(a.cmid, a.cexp, a.c1, a.M) || a.x2 || a.cds || !a.x || !a.res || !a.w3 || !a.b3 || !a.w1 ||
       !a.b1 || !a.y || !a.z)
     return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
-  if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128>(a, s);
-  if (a.cmid == 128) return launch_pairw<128, 512, 256>(a, s);
-  return launch_pairw<256, 1024, 256>(a, s);
+  if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128, 1>(a, s);
+  if (a.cmid == 128) return launch_pairw<128, 512, 256, 1>(a, s);
+  return launch_pairw<256, 1024, 256, 1>(a, s);
 }
 
 }  // namespace eosv

@@ -615,6 +615,8 @@ int main() {
   fails += check_bf16(3, 7, 7, 512, 512, 3, 1, 1, false, true, true);
   fails += check_bf16(2, 9, 11, 128, 128, 3, 1, 1, true, false, true);
   fails += check_bf16(7, 56, 56, 64, 128, 3, 2, 1, false, true);
+  fails += check_bf16(5, 56, 56, 128, 128, 3, 2, 1, false, true, true);  // R50 layer2.0.conv2 (kcm)
+  fails += check_bf16(3, 13, 11, 64, 128, 3, 2, 1, false, true);         // ragged stride-2 entry, M tail
   fails += check_bf16(7, 56, 56, 64, 128, 1, 2, 0, false, false);
   fails += check_bf16(30, 14, 14, 256, 256, 3, 1, 1, true, true);
   fails += check_bf16(9, 28, 28, 128, 256, 3, 2, 1, false, true);

@@ -70,23 +70,45 @@ def config3(args):
                 "kernel": f"conv family: {int(nl.sum())} conv launches of the timed region, summed algorithmic "
                           "FLOPs / summed HIP-event durations",
                 "conv_share_of_wall": round(conv_ms * 1e-3 / el, 3)}
-    cpu = None
+    cpu = parity = None
     if args.cpu_episodes:
-        cpu = c3_cpu_baseline(tn, gal, plans[:args.cpu_episodes], preds[:args.cpu_episodes])
+        cpu, parity = c3_cpu_baseline(tn, gal, plans[:args.cpu_episodes], preds[:args.cpu_episodes])
     acc = float(np.mean([p == q["query_y"] for p, q in zip(preds, plans)]))
+    roofline["traffic"], roofline["traffic_source"] = c3_traffic(args.dtype)
+    roofline["traffic_unit"] = "HBM bytes per conv launch (PMC)"
     reforward = os.environ.get("EOSV_AUG_REFORWARD", "0") == "1"
     # backbone frames per episode: query (<=16) + 5 supports x 16 (+ 40 augmented clips x 16 when
     # they are re-forwarded as the reference does; by default their features are gathered)
     frames_ep = 16 + 5 * 16 + (40 * 16 if reforward else 0)
     gflop = 2 * arch.conv_macs_per_frame(arch.SPECS["resnet50"]) / 1e9
-    return {"config": "3: test_network_aug_segment aug_seg_T 5w1s R50 224 (drop-in TestNetwork)",
+    fps = round(args.episodes * frames_ep / el, 1)
+    return {"metric": "config-3 backbone frames/s (aug_seg_T 5-way 1-shot, R50, 224x224)",
+            # the work rate: frames that go through the backbone (the 40 augmented clips per episode are
+            # assembled from already-computed frame features unless EOSV_AUG_REFORWARD=1)
+            "value": fps, "unit": "backbone frames/s",
+            "config": "3: test_network_aug_segment aug_seg_T 5w1s R50 224 (drop-in TestNetwork)",
             "dtype": args.dtype, "aug_features": "reforward" if reforward else "gathered",
             "episodes": args.episodes, "batch": B, "episodes_per_s": round(args.episodes / el, 2),
             "clips_per_s": round(args.episodes * 46 / el, 1),
-            "backbone_frames_per_episode": frames_ep, "backbone_frames_per_s": round(args.episodes * frames_ep / el, 1),
+            "clips_per_s_note": "46 clips per episode (5 supports + 40 augmented + 1 query); only "
+                                f"{frames_ep} frames per episode go through the backbone",
+            "backbone_frames_per_episode": frames_ep, "backbone_frames_per_s": fps,
             "end_to_end_tflops": round(args.episodes * frames_ep * gflop / el / 1e3, 1),
             "gallery_s": round(t_gal, 3), "gallery_frames": 10240, "episode_acc": acc,
-            "roofline": roofline, "cpu_baseline": cpu}
+            "roofline": roofline, "cpu_baseline": cpu, "cpu_parity": parity}
+
+
+def c3_traffic(dtype):
+    """HBM bytes per conv launch from the newest profiles/*_c3_traffic.json of this workload and
+    these kernel sources (tools/traffic_json.py over the config-3 PMC passes), else None."""
+    import glob
+
+    from eosv._lib import source_digest
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*c3*_traffic.json")), reverse=True):
+        d = json.load(open(path))
+        if d.get("key") == "c3:resnet50@224x224" and d.get("src_sha16") == source_digest() and dtype in d:
+            return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, None
 
 
 def c3_cpu_baseline(tn, gal, plans, gpu_preds):
@@ -132,22 +154,27 @@ def c3_cpu_baseline(tn, gal, plans, gpu_preds):
         t += time.perf_counter() - t0
         equal += int(int(r["pred"][0]) == int(gp))
     n = len(plans)
-    return {"value": round(n / t, 4), "unit": "episodes/s", "cores": threads, "kind": "port",
+    base = {"value": round(n / t, 4), "unit": "episodes/s", "cores": threads, "kind": "port",
+            "value_backbone_frames_per_s": round(n * (16 + 5 * 16 + 40 * 16) / t, 2),
             "sample": f"{n} aug_seg_T episodes through oracle/harness_ref.aug_segment_episode (R50 fp32 torch-CPU, "
-                      f"gallery features from the GPU run, frame synthesis included); {t:.1f}s",
-            "pred_equal_vs_gpu_leg": f"{equal}/{n}"}
+                      f"the reference's 736 backbone frames per episode, gallery features from the GPU run, "
+                      f"frame synthesis included); {t:.1f}s"}
+    parity = {"episodes": n, "pred_equal": equal, "against": "the GPU leg's predictions on the same episodes"}
+    return base, parity
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--dtype", default="bf16")
-    ap.add_argument("--episodes", type=int, default=64)
+    ap.add_argument("--episodes", type=int, default=0, help="per step (default: 64 config 3, 40 config 4, 8 config 5)")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-episodes", type=int, default=0, help="config 3: oracle episodes for cpu_baseline")
+    ap.add_argument("--steps", type=int, default=5, help="configs 4 / 5: timed steps of --episodes episodes")
+    ap.add_argument("--cpu-episodes", type=int, default=2, help="config 3: oracle episodes for cpu_baseline (0: none)")
     ap.add_argument("--max-frames", type=int, default=0, help="backbone chunk (default: 4096 config 3, 2048 configs 4 / 5)")
     args = ap.parse_args()
+    args.episodes = args.episodes or {3: 64, 4: 40, 5: 8}[args.config]
     if args.config == 3:
         print(json.dumps(config3(args)), flush=True)
         return
@@ -156,7 +183,7 @@ def main():
                  "--list", os.path.join(REPO, "tests", "golden", "unreal14.list")],
              5: ["--arch", "resnet101", "--n-way", "5", "--k-shot", "5", "--segments", "32", "--res", "256"]}[args.config]
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), *shape, "--dtype", args.dtype,
-           "--episodes-per-step", str(args.episodes), "--steps", "2", "--secondary-dtype", "",
+           "--episodes-per-step", str(args.episodes), "--steps", str(args.steps), "--secondary-dtype", "",
            "--cpu-baseline-sec", "10",
            "--max-frames", str(args.max_frames or 2048), "--config-label", f"BASELINE configs[{args.config - 1}]"]
     sys.exit(subprocess.call(cmd))
