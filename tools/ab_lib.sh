@@ -11,7 +11,7 @@ if [ -n "$CHECK" ]; then
 fi
 for arm in base new base new; do
   if [ $arm = base ]; then cp tools/ablib/libeosv_base.so $LIB; else cp /tmp/libeosv_new.so $LIB; fi
-  timeout -k 10 200 python bench.py --dtype ${DTYPE:-bf16} --secondary-dtype none --no-cpu-baseline --layers --steps ${STEPS:-3} \
+  timeout -k 10 200 python bench.py --arch ${ARCH:-resnet18} --dtype ${DTYPE:-bf16} --secondary-dtype none --no-cpu-baseline --layers --steps ${STEPS:-3} \
     > gpurun_out/ab_lib.json 2> gpurun_out/ab_lib_$arm.err || { tail gpurun_out/ab_lib_$arm.err; cp /tmp/libeosv_new.so $LIB; exit 1; }
   echo "[$arm] $(python -c "import json;d=json.load(open('gpurun_out/ab_lib.json'));print(d['value'], d['roofline']['achieved'])")"
   grep -E "layer +(${LAYERS:-0|1|5|6|8|9|10|11|13|14|15|16|18|19}):" gpurun_out/ab_lib_$arm.err | awk '{printf "%s%s ", $3, $4} END {print ""}'

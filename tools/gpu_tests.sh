@@ -1,7 +1,10 @@
 #!/bin/bash
+# the whole GPU suite + smoke (as the driver runs them), durations of the slowest tests
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread --durations 15 -rs ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -40 gpurun_out/pytest_gpu.log
-exit $rc
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -2 gpurun_out/smoke.log; exit $rc
