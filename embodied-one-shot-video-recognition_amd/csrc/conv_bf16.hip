@@ -218,6 +218,52 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
     constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
+    if constexpr (MF == 16) {
+      if (!(EOSV_ABL(a) & (16 | 32))) {
+        // Software-pipelined fragment reads (r03): the K-step's MFMAs go in groups (slice s, A row
+        // tile i) of TN MFMAs; the next group's A fragment (and at a slice boundary the next
+        // slice's TN B fragments) are read from LDS while this group's MFMAs run, instead of
+        // waiting lgkmcnt(0) on fresh reads before every group (SQ_WAIT_INST_ANY 0.36 on the
+        // 256x256 tile, r02z).  Same MFMAs in the same per-accumulator order: bit-identical.
+        constexpr int NSL = BK / KS, NG = NSL * TM;
+        bf16x8 bfr[2][TN], afr[2];
+        auto rdA = [&](int g) {
+          const int s = g / TM, i = g - (g / TM) * TM;
+          return *(const bf16x8*)(As + (wm * (BM / WM) + i * MF + r) * BK + ((s * (KS / 8) + q) ^ sw) * 8);
+        };
+        auto rdB = [&](int s, bf16x8* f) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            f[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * MF + r) * BK + ((s * (KS / 8) + q) ^ sw) * 8);
+        };
+        rdB(0, bfr[0]);
+        afr[0] = rdA(0);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const int s = g / TM, i = g - (g / TM) * TM;
+          int nrd = 0;
+          if (g + 1 < NG) {
+            if ((g + 1) % TM == 0) {
+              rdB((g + 1) / TM, bfr[((g + 1) / TM) & 1]);
+              nrd += TN;
+            }
+            afr[(g + 1) & 1] = rdA(g + 1);
+            nrd += 1;
+          }
+          // order: this group's first MFMA (hipcc's lgkmcnt wait for this group's fragments goes
+          // before it), then the next group's reads, then the other MFMAs: the reads are not
+          // covered by that wait and overlap this group's MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (nrd == TN + 1) __builtin_amdgcn_sched_group_barrier(0x100, TN + 1, 0);
+          if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[g & 1], bfr[s & 1][j], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else
 #pragma unroll
     for (int s = 0; s < BK / KS; ++s) {
       const int pch = ((s * (KS / 8) + q) ^ sw) * 8;
