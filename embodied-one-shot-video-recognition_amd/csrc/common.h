@@ -154,12 +154,15 @@ struct Pair1x1Args {
   int c1, cds;
   LaunchInfo* plan;  // non-null: record the grid only
   int cmid, cexp;    // pairw_bf16: conv3 is 1x1 cmid -> cexp, the next conv1 cexp -> c1
+  // pairw_bf16 with the downsample (cds > 0): x2 is [N][H2][W2][cds], read at (2 oh, 2 ow) of
+  // output pixel (n, oh, ow) of the Ho x Wo map
+  int Ho, Wo, H2, W2;
 };
 bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
 // pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
 // streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
-bool pairw_bf16_ok(int cmid, int cexp, int c1, long long M);
+bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);

@@ -491,16 +491,22 @@ static bool pairw_enabled() {
 static bool pair_ok(const eosv_handle* h, const Block& b, const Block* nb, long long M) {
   if (!pair_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || !nb || !nb->bottleneck) return false;
   const Conv &c3 = b.c3, &n1 = nb->c1;
-  if (b.c2.stride != 1 || c3.kh != 1 || n1.kh != 1 || n1.stride != 1 || n1.cin != c3.cout) return false;
-  if (b.has_ds && !(b.fuse_ds && b.ds.stride == 1)) return false;
-  if (c3.cin != 64) return pairw_enabled() && !b.has_ds && pairw_bf16_ok(c3.cin, c3.cout, n1.cout, M);
+  if (c3.kh != 1 || n1.kh != 1 || n1.stride != 1 || n1.cin != c3.cout) return false;
+  if (c3.cin != 64) {
+    // the stage's block 0: conv3 + the folded stride-2 downsample (a fused-ds block whose 3x3 has
+    // stride 2), or a plain residual block
+    const bool ds = b.has_ds && b.fuse_ds && b.ds.stride == 2 && b.c2.stride == 2;
+    if (!pairw_enabled() || (b.has_ds && !ds)) return false;
+    return pairw_bf16_ok(c3.cin, c3.cout, n1.cout, ds ? c3.kds : 0, M);
+  }
+  if (b.c2.stride != 1 || (b.has_ds && !(b.fuse_ds && b.ds.stride == 1))) return false;
   return pair1x1_bf16_ok(c3.cin, c3.cout, n1.cout, b.has_ds ? c3.kds : 0, M);
 }
 
 // conv3 of `b` (+ residual `res` or the folded downsample reading x2) -> y, and the next block's
 // conv1 on y -> z, in one launch; profiled as conv3's layer with both convs' FLOPs
 static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void* x, const void* x2, const void* res,
-                    void* y, void* z, long long M, hipStream_t s) {
+                    void* y, void* z, long long M, hipStream_t s, int ho = 0, int wo = 0, int hin = 0, int win = 0) {
   Pair1x1Args p{};
   p.x = x;
   p.x2 = x2;
@@ -516,6 +522,10 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
   p.cds = x2 ? b.c3.kds : 0;
   p.cmid = b.c3.cin;
   p.cexp = b.c3.cout;
+  p.Ho = ho;
+  p.Wo = wo;
+  p.H2 = hin;
+  p.W2 = win;
   const bool wide = p.cmid != 64;
   const double flops = 2.0 * M * ((double)b.c3.cout * (b.c3.cin + p.cds) + (double)nb.c1.cout * nb.c1.cin);
   if (h->planning) {
@@ -579,7 +589,7 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
       const long long M = (long long)B * ho * wo;
       c1_done = pair_ok(h, b, nb, M) && y != dst && z != x && z != fr[1];
       if (c1_done) {
-        if ((rc = run_pair(h, b, *nb, fr[1], x2, res, y, z, M, s))) return rc;
+        if ((rc = run_pair(h, b, *nb, fr[1], x2, res, y, z, M, s, ho, wo, hh, ww))) return rc;
       } else if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) {
         return rc;
       }

@@ -62,11 +62,15 @@ constexpr int PW_TILE = 128;  // pixels per round
 // NPT: 16-pixel tiles per wave.  NPT = 1: 8 waves (two per SIMD); NPT = 2: 4 waves (one per SIMD,
 // 512 VGPRs) that read each LDS weight fragment once for 32 pixels -- the LDS feeds one fragment per
 // MFMA at NPT = 1, which at CMID 256 made the weight reads, not HBM, the pair's limit.
-template <int CMID, int CEXP, int C1, int NPT>
+// DSC > 0 (block 0 of a stage, r03): conv3's K also holds the folded stride-2 1x1 downsample, DSC
+// more columns read from the previous stage's output x2 at pixel (2 oh, 2 ow) (ConvArgs::x2 of
+// the unfused conv), and there is no residual.
+template <int CMID, int CEXP, int C1, int NPT, int DSC = 0>
 struct PairW {
+  static constexpr int K3 = CMID + DSC;                // conv3's K
   static constexpr int NW = 8 / NPT;                   // waves per workgroup
   static constexpr int PX = 16 * NPT;                  // pixels per wave
-  static constexpr int W3B = 64 * CMID * 2;  // a chunk's W3 rows (64 couts x CMID), bytes
+  static constexpr int W3B = 64 * K3 * 2;  // a chunk's W3 rows (64 couts x K3), bytes
   static constexpr int W1B = C1 * 64 * 2;    // a chunk's W1 columns (C1 x 64 k), bytes
   static constexpr int STAGE_W = W3B + W1B;
   // + the chunk's 64 conv3 BN shifts (256 B, DMA'd with the weights: an LDS read outside the ring
@@ -74,7 +78,8 @@ struct PairW {
   static constexpr int STAGE = STAGE_W + 256;
   static constexpr int PPW = STAGE_W / 1024 / NW;  // 1-KiB DMA pieces per wave per chunk
   static constexpr int NCH = CEXP / 64;
-  static constexpr int XS = CMID / 32;  // X fragments (k-slices of GEMM1) per lane
+  static constexpr int XS = K3 / 32;    // X fragments (k-slices of GEMM1) per lane
+  static constexpr int XSM = CMID / 32;  // ... of them from x (the rest from x2)
   static constexpr int G2 = C1 / 64;    // 64-cout groups of GEMM2
   static constexpr int LDS = 2 * STAGE + C1 * 4;
   static_assert(STAGE_W % (1024 * NW) == 0 && W3B % 1024 == 0 && PPW >= 2, "DMA pieces");
@@ -82,9 +87,10 @@ struct PairW {
   static_assert(PPW < XS + 2 * G2, "DMA pieces go out one per fragment group, the residual loads after them");
 };
 
-template <int CMID, int CEXP, int C1, int NPT>
+template <int CMID, int CEXP, int C1, int NPT, int DSC>
 __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a) {
-  using P = PairW<CMID, CEXP, C1, NPT>;
+  using P = PairW<CMID, CEXP, C1, NPT, DSC>;
+  constexpr int K3 = P::K3, XSM = P::XSM;
   constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW, NT = 64 * P::NW;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS];
   float* const b1s = (float*)(smem + 2 * P::STAGE);
@@ -108,9 +114,9 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   for (int j = 0; j < PPW; ++j) {
     const int o = (w * PPW + j) * 1024 + lane * 16;
     if (o < P::W3B) {  // W3 row R (tile R >> 4, row R & 15), 16-B chunk c' = c ^ (R & 15)
-      const int R = o / (CMID * 2), cs = (o % (CMID * 2)) / 16;
+      const int R = o / (K3 * 2), cs = (o % (K3 * 2)) / 16;
       const int c = cs ^ (R & 15);
-      vrel[j] = (permrow(R >> 4, R & 15) * CMID + 8 * c) * 2;
+      vrel[j] = (permrow(R >> 4, R & 15) * K3 + 8 * c) * 2;
     } else {  // W1 row RR (group RR >> 6, tile (RR >> 4) & 3, row RR & 15), c' = c ^ ((RR >> 1) & 7)
       const int o1 = o - P::W3B;
       const int RR = o1 / 128, cs = (o1 % 128) / 16;
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
     const int o = (w * PPW + j) * 1024;  // wave-uniform
     unsigned char* dst = smem + slot * P::STAGE + o;
     if (o < P::W3B)
-      dma16(w3b + (long long)ch * 64 * CMID * 2 + vrel[j], dst);
+      dma16(w3b + (long long)ch * 64 * K3 * 2 + vrel[j], dst);
     else
       dma16(w1b + ch * 128 + vrel[j], dst);
     if (j == 0 && w == 0 && lane < 16)  // the chunk's conv3 shifts: 16 lanes x 16 B
@@ -145,12 +151,27 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   };
   // the lane's pixels within a round: 16 t + r of the wave's block, t < NPT
   const int pw = P::PX * w + r;
-  auto load_x = [&](const RoundRes& rr, v4u (*xf)[XS]) {
+  // DSC: x2 pixel (img, 2 oh, 2 ow) of the lane's pixel p of round t (tails: pixel 0, never stored)
+  auto x2pix = [&](long long t, int tt) {
+    long long p = t * PW_TILE + pw + 16 * tt;
+    if (p >= M) p = 0;
+    const long long hw = (long long)a.Ho * a.Wo;
+    const long long img = p / hw;
+    const int rem = (int)(p - img * hw), oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+    return (const unsigned short*)a.x2 + ((img * a.H2 + 2 * oh) * a.W2 + 2 * ow) * DSC + 8 * q;
+  };
+  auto load_x = [&](const RoundRes& rr, long long t, v4u (*xf)[XS]) {
 #pragma unroll
-    for (int t = 0; t < NPT; ++t)
+    for (int tt = 0; tt < NPT; ++tt) {
 #pragma unroll
-      for (int s = 0; s < XS; ++s)
-        xf[t][s] = __builtin_amdgcn_raw_buffer_load_b128(rr.x, ((pw + 16 * t) * CMID + 8 * q) * 2, 64 * s, 0);
+      for (int s = 0; s < XSM; ++s)
+        xf[tt][s] = __builtin_amdgcn_raw_buffer_load_b128(rr.x, ((pw + 16 * tt) * CMID + 8 * q) * 2, 64 * s, 0);
+      if constexpr (DSC > 0) {
+        const unsigned short* p2 = x2pix(t, tt);
+#pragma unroll
+        for (int s = XSM; s < XS; ++s) xf[tt][s] = *(const v4u*)(p2 + 32 * (s - XSM));
+      }
+    }
   };
   auto load_r = [&](const RoundRes& rr, int ch, v4u (*rv)[2]) {
 #pragma unroll
@@ -164,13 +185,16 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   // the residual of chunk ch is loaded RD chunks ahead (HBM latency under load is several chunks
   // of this loop: with one chunk of lead the epilogue waited on it), into a ring of 4 register sets
   constexpr int RD = XS >= 8 ? 2 : 3;  // (CMID 256: one set fewer keeps the wave within 256 VGPRs)
+  constexpr int NRES = DSC ? 0 : 2 * NPT;  // residual loads per chunk
   RoundRes cur = round_res(rt);
   v4u xf[NPT][XS], rres[4][NPT][2];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) dma_piece(j, 0, 0);
-  load_x(cur, xf);
+  load_x(cur, rt, xf);
+  if constexpr (!DSC) {
 #pragma unroll
-  for (int c = 0; c < RD; ++c) load_r(cur, c, rres[c]);
+    for (int c = 0; c < RD; ++c) load_r(cur, c, rres[c]);
+  }
 
   for (; rt < nrounds; rt += gridDim.x) {
     const RoundRes nxt = round_res(rt + gridDim.x);
@@ -198,9 +222,9 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       // next round's XS NPT X loads when the epilogue (after group XS - 1) follows the last piece,
       // and the last chunk's 2 G2 NPT Z stores; before the loop: XS NPT X loads + 2 RD NPT residual
       // loads after the pieces.
-      constexpr int YOUNG = 2 * NPT + (XS >= PPW ? 2 * NPT : 0);
+      constexpr int YOUNG = NRES + (XS >= PPW ? 2 * NPT : 0);
       constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0) + 2 * G2 * NPT;
-      constexpr int YOUNG_PRO = (XS + 2 * RD) * NPT;
+      constexpr int YOUNG_PRO = XS * NPT + (DSC ? 0 : 2 * RD * NPT);
       if (u == 0)
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST) : "memory");
       else
@@ -219,7 +243,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       auto frags = [&](int gi, bf16x8* f) {
         if (gi < XS) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) f[i] = *(const bf16x8*)(ws + (16 * i + r) * (CMID * 2) + (((4 * gi + q) ^ r) << 4));
+          for (int i = 0; i < 4; ++i) f[i] = *(const bf16x8*)(ws + (16 * i + r) * (K3 * 2) + (((4 * gi + q) ^ r) << 4));
         } else {
           const int s2 = (gi - XS) / G2, g = (gi - XS) % G2;
 #pragma unroll
@@ -240,7 +264,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
         if (gi < PPW) dma_piece(gi, nch, slot ^ 1);
-        if (gi == PPW) {  // branch-free (scalar selects): a branch here made hipcc wait vmcnt(0) at the join
+        if (!DSC && gi == PPW) {  // branch-free (scalar selects): a branch here made hipcc wait vmcnt(0) at the join
           const bool here = ch + RD < NCH;
           RoundRes rr;
           rr.res = here ? cur.res : nxt.res;
@@ -270,7 +294,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
         __builtin_amdgcn_sched_barrier(0);
         if (gi == XS - 1) {
           if (u == 3 && cp + 4 == NCH) {  // the round's X is dead: the next round's goes into the same registers
-            load_x(nxt, xf);
+            load_x(nxt, rt + gridDim.x, xf);
             __builtin_amdgcn_sched_barrier(0);
           }
           // epilogue 1: + shift, + residual, ReLU, bf16 -> Y (global) and the GEMM2 B fragments
@@ -285,15 +309,17 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
             const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
 #pragma unroll
             for (int t = 0; t < NPT; ++t) {
-              const v4u rv = rres[u][t][hh];  // ring slot ch & 3
+              const v4u rv = DSC ? v4u{0, 0, 0, 0} : rres[u][t][hh];  // ring slot ch & 3 (no residual with DSC)
               v4u pk;
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
                 const int e0 = 2 * k, e1 = 2 * k + 1;  // elements of the lane's 8 couts
                 float v0 = acc1[t][2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
                 float v1 = acc1[t][2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-                v0 += lo_f(rv[k]);
-                v1 += hi_f(rv[k]);
+                if constexpr (!DSC) {
+                  v0 += lo_f(rv[k]);
+                  v1 += hi_f(rv[k]);
+                }
                 pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
               }
               __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2,
@@ -328,26 +354,28 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) chunk-0 prefetch has landed
 }
 
-template <int CMID, int CEXP, int C1, int NPT>
+template <int CMID, int CEXP, int C1, int NPT, int DSC = 0>
 static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
-  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT>, 512 / NPT);
+  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC>, 512 / NPT);
   const long long nrounds = (a.M + PW_TILE - 1) / PW_TILE;
   if (a.plan) return record_launch(a.plan, nrounds, occ);
   const long long grid = std::min<long long>(nrounds, (long long)occ * device_cu_count());
-  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
+  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
 
-bool pairw_bf16_ok(int cmid, int cexp, int c1, long long M) {
+bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M) {
   if (M <= 0) return false;
+  if (cds) return cmid == 128 && cexp == 512 && c1 == 128 && cds == 256;  // stage-2 block 0
   return (cmid == 128 && cexp == 512 && (c1 == 128 || c1 == 256)) || (cmid == 256 && cexp == 1024 && c1 == 256);
 }
 
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
-  if (!pairw_bf16_ok(a.cmid, a.cexp, a.c1, a.M) || a.x2 || a.cds || !a.x || !a.res || !a.w3 || !a.b3 || !a.w1 ||
-      !a.b1 || !a.y || !a.z)
+  if (!pairw_bf16_ok(a.cmid, a.cexp, a.c1, a.cds, a.M) || !a.x || !a.w3 || !a.b3 || !a.w1 || !a.b1 || !a.y || !a.z ||
+      (a.cds ? (!a.x2 || a.res || a.Ho <= 0 || a.Wo <= 0 || a.H2 < 2 * a.Ho - 1 || a.W2 < 2 * a.Wo - 1) : (!a.res || a.x2)))
     return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
+  if (a.cds) return launch_pairw<128, 512, 128, 1, 256>(a, s);
   if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128, 1>(a, s);
   if (a.cmid == 128) return launch_pairw<128, 512, 256, 1>(a, s);
   return launch_pairw<256, 1024, 256, 1>(a, s);

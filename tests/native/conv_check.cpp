@@ -508,19 +508,24 @@ static int check_pair(int N, int H, int W, int c1, bool ds) {
 // wide bottleneck pair (pairw_bf16.hip, stages 2-3) vs the unfused conv3 (1x1 cmid -> cexp +
 // residual) -> conv1 (1x1 cexp -> c1) through launch_conv_bf16: both maps bit-identical.  M
 // need not be a multiple of the 128-pixel round (tail pixels read zeros, their stores dropped).
-static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1) {
+static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds = 0) {
+  // cds > 0: block 0 of a stage, conv3 + the folded stride-2 downsample reading x2 [N][2H][2W][cds]
+  // (ragged: 2H - 1 when odd sizes are asked for through H2/W2 below), no residual
   const long long M = (long long)N * H * W;
+  const int H2 = 2 * H, W2 = 2 * W;
+  const int K3 = cmid + cds;
   unsigned s = 4242 + cmid + c1;
   auto fill = [&](std::vector<unsigned short>& v, float scale) {
     for (auto& e : v) e = f2bf(frand(s) * scale);
   };
-  std::vector<unsigned short> x(M * cmid), res(M * cexp), w3((size_t)cexp * cmid), w1((size_t)c1 * cexp);
-  fill(x, 1.f); fill(res, 1.f); fill(w3, 0.125f); fill(w1, 0.0625f);
+  std::vector<unsigned short> x(M * cmid), res(M * cexp), w3((size_t)cexp * K3), w1((size_t)c1 * cexp);
+  std::vector<unsigned short> x2(cds ? (size_t)N * H2 * W2 * cds : 1);
+  fill(x, 1.f); fill(res, 1.f); fill(w3, 0.125f); fill(w1, 0.0625f); fill(x2, 1.f);
   std::vector<float> b3(cexp), b1(c1);
   for (auto& v : b3) v = frand(s) * 0.5f;
   for (auto& v : b1) v = frand(s) * 0.5f;
   auto up = [](const void* p, size_t n) { void* d; hipMalloc(&d, n); hipMemcpy(d, p, n, hipMemcpyHostToDevice); return d; };
-  void *dx = up(x.data(), x.size() * 2), *dr = up(res.data(), res.size() * 2);
+  void *dx = up(x.data(), x.size() * 2), *dr = up(res.data(), res.size() * 2), *dx2 = up(x2.data(), x2.size() * 2);
   void *dw3 = up(w3.data(), w3.size() * 2), *dw1 = up(w1.data(), w1.size() * 2);
   float *db3 = (float*)up(b3.data(), b3.size() * 4), *db1 = (float*)up(b1.data(), b1.size() * 4);
   void *y0, *z0, *y1, *z1, *dz;
@@ -528,9 +533,10 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1) {
   hipMemset(y1, 0xff, M * cexp * 2); hipMemset(z1, 0xff, M * c1 * 2);
   hipMalloc(&dz, 256); hipMemset(dz, 0, 256);
   ConvArgs a{};
-  a.x = dx; a.w = dw3; a.bias = db3; a.res = dr; a.y = y0;
+  a.x = dx; a.w = dw3; a.bias = db3; a.res = cds ? nullptr : dr; a.y = y0;
   a.N = N; a.H = H; a.W = W; a.Cin = cmid; a.Ho = H; a.Wo = W; a.Cout = cexp;
-  a.KH = a.KW = a.KWp = 1; a.stride = 1; a.pad = 0; a.K = cmid; a.relu = 1; a.zero = dz; a.xcd = 1;
+  a.KH = a.KW = a.KWp = 1; a.stride = 1; a.pad = 0; a.K = K3; a.relu = 1; a.zero = dz; a.xcd = 1;
+  if (cds) { a.x2 = dx2; a.H2 = H2; a.W2 = W2; a.Cin2 = cds; a.stride2 = 2; a.K1 = cmid; }
   int rc = launch_conv_bf16(a, 0);
   ConvArgs b{};
   b.x = y0; b.w = dw1; b.bias = db1; b.res = nullptr; b.y = z0;
@@ -538,8 +544,9 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1) {
   b.KH = b.KW = b.KWp = 1; b.stride = 1; b.pad = 0; b.K = cexp; b.relu = 1; b.zero = dz; b.xcd = 1;
   rc |= launch_conv_bf16(b, 0);
   Pair1x1Args p{};
-  p.x = dx; p.res = dr; p.w3 = dw3; p.b3 = db3; p.w1 = dw1; p.b1 = db1;
+  p.x = dx; p.res = cds ? nullptr : dr; p.w3 = dw3; p.b3 = db3; p.w1 = dw1; p.b1 = db1;
   p.y = y1; p.z = z1; p.M = M; p.c1 = c1; p.cmid = cmid; p.cexp = cexp;
+  if (cds) { p.x2 = dx2; p.cds = cds; p.Ho = H; p.Wo = W; p.H2 = H2; p.W2 = W2; }
   const int rcp = launch_pairw_bf16(p, 0);
   hipDeviceSynchronize();
   std::vector<unsigned short> hy0(M * cexp), hy1(M * cexp), hz0(M * c1), hz1(M * c1);
@@ -555,14 +562,21 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1) {
   for (long long m = 0; m < M; m += M / 7 + 1)
     for (int o = 0; o < cexp; o += 7) {
       double acc = b3[o];
-      for (int k = 0; k < cmid; ++k) acc += (double)bf2f(x[m * cmid + k]) * bf2f(w3[(size_t)o * cmid + k]);
-      acc = std::max(acc + bf2f(res[m * cexp + o]), 0.0);
+      for (int k = 0; k < cmid; ++k) acc += (double)bf2f(x[m * cmid + k]) * bf2f(w3[(size_t)o * K3 + k]);
+      if (cds) {
+        const long long n = m / (H * W), rem = m % (H * W), oh = rem / W, ow = rem % W;
+        const size_t p2 = (size_t)((n * H2 + 2 * oh) * W2 + 2 * ow) * cds;
+        for (int k = 0; k < cds; ++k) acc += (double)bf2f(x2[p2 + k]) * bf2f(w3[(size_t)o * K3 + cmid + k]);
+      } else {
+        acc += bf2f(res[m * cexp + o]);
+      }
+      acc = std::max(acc, 0.0);
       maxerr = std::max(maxerr, fabs(acc - bf2f(hy0[m * cexp + o])) / (1.0 + fabs(acc)));
     }
   const bool fail = rc || rcp || bady || badz || maxerr > 1e-2;
-  printf("%s pairw bf16 N%d H%d W%d %d->%d->%d M%lld rc=%d/%d differing y %ld z %ld (max %.3e) unfused maxerr %.3e\n",
-         fail ? "FAIL" : "ok  ", N, H, W, cmid, cexp, c1, M, rc, rcp, bady, badz, maxd, maxerr);
-  for (void* q : {dx, dr, dw3, dw1, (void*)db3, (void*)db1, y0, y1, z0, z1, dz}) hipFree(q);
+  printf("%s pairw bf16 N%d H%d W%d %d(+ds %d)->%d->%d M%lld rc=%d/%d differing y %ld z %ld (max %.3e) unfused maxerr %.3e\n",
+         fail ? "FAIL" : "ok  ", N, H, W, cmid, cds, cexp, c1, M, rc, rcp, bady, badz, maxd, maxerr);
+  for (void* q : {dx, dr, dx2, dw3, dw1, (void*)db3, (void*)db1, y0, y1, z0, z1, dz}) hipFree(q);
   return fail ? 1 : 0;
 }
 
@@ -575,6 +589,9 @@ int main() {
   fails += check_pairw(3, 14, 14, 256, 1024, 256);
   fails += check_pairw(200, 14, 14, 256, 1024, 256);
   fails += check_pairw(1, 7, 5, 128, 512, 128);
+  // stage-2 block 0: conv3 + the folded stride-2 downsample (x2 = the 56x56x256 stage-1 output)
+  fails += check_pairw(40, 28, 28, 128, 512, 128, 256);
+  fails += check_pairw(3, 7, 5, 128, 512, 128, 256);
   // R50 layer1 pairs: block 1/2 (residual, c1 64), block 0 (downsample), layer1 -> layer2 (c1 128);
   // 700 images = 34300 tiles (~134 per workgroup), 64-wide maps (R101 @ 256)
   fails += check_pair(700, 56, 56, 64, false);
