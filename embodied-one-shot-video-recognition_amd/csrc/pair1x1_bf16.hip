@@ -70,6 +70,17 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
   u16* __restrict__ y = (u16*)a.y;
   u16* __restrict__ z = (u16*)a.z;
 
+  // folded-BN shifts of this lane's channels (loaded first: the weight copy's waits retire them,
+  // so none is left to wait for inside the tile loop): element k <-> channel 32(k >> 3) + 8q + (k & 7) of
+  // the 64-cout group (conv3: group w, conv1: group g)
+  float b3v[16], b1v[G2][16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) b3v[k] = a.b3[64 * w + 32 * (k >> 3) + 8 * q + (k & 7)];
+#pragma unroll
+  for (int g = 0; g < G2; ++g)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b1v[g][k] = a.b1[64 * g + 32 * (k >> 3) + 8 * q + (k & 7)];
+
   // weights -> LDS once (rows of K3 / 256 bf16, 16-B chunks swizzled)
   {
     const u16* w3 = (const u16*)a.w3;
@@ -83,16 +94,6 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
       *(v4u*)(W1s + row * 256 + swz(row, c)) = *(const v4u*)(w1 + (long long)row * 256 + c * 8);
     }
   }
-  // folded-BN shifts of this lane's channels: element k <-> channel 32(k >> 3) + 8q + (k & 7) of
-  // the 64-cout group (conv3: group w, conv1: group g)
-  float b3v[16], b1v[G2][16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) b3v[k] = a.b3[64 * w + 32 * (k >> 3) + 8 * q + (k & 7)];
-#pragma unroll
-  for (int g = 0; g < G2; ++g)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) b1v[g][k] = a.b1[64 * g + 32 * (k >> 3) + 8 * q + (k & 7)];
-
   // X (and the downsample's input) of tile t: thread chunk k -> pixel (tid + 256k) / 8 mod 64
   v4u xr[XL];
   auto load_x = [&](long long tt) {
@@ -127,16 +128,19 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
   };
   load_x(t);
   load_r(t);
+  store_x();
   const float rlow = 0.f;  // both convs end in ReLU
 
   for (; t < ntiles; t += gridDim.x) {
     const long long p0 = t * BM;
-    const long long tn = t + gridDim.x;
-    store_x();
+    // the next tile (the last one again past the end: branch-free, so the compiler counts the
+    // loads in flight instead of draining them at the join)
+    const long long tn = t + gridDim.x < ntiles ? t + gridDim.x : ntiles - 1;
     // (A): X tile (and, first time round, the weights) in LDS; the previous tile's GEMM2 is done with Ys
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (tn < ntiles) load_x(tn);
+    load_x(tn);
+    __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk below GEMM1
 
     // GEMM1: wave w, couts 64w + (tile i, row 4q' + e -> 32(i >> 1) + 8q' + 4(i & 1) + e), pixels 16j + r
     f32x4 acc[4][4];
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
         *(v4u*)(Ys + prow * 256 + swz(prow, c0 / 8 + 4 * hh)) = pk[hh];
       }
     }
-    if (tn < ntiles) load_r(tn);
+    load_r(tn);
     // (B): Ys complete; every wave is done reading Xs
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -222,6 +226,11 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
           acc2[g][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, by, acc2[g][i], 0, 0, 0);
         }
     }
+    // the next X tile -> Xs (free since (B)), here rather than at the loop head: hipcc counts only
+    // loads in vmcnt, so at the head its wait for X also drained this tile's Z stores
+    __builtin_amdgcn_sched_barrier(0);
+    store_x();
+    __builtin_amdgcn_sched_barrier(0);
     // epilogue 2: + shift, ReLU, bf16 -> Z
     {
       const long long p = p0 + 16 * w + r;
