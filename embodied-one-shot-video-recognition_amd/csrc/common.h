@@ -10,6 +10,16 @@
 
 namespace eosv {
 
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt split over bits 3:0 and 15:14, expcnt / lgkmcnt left
+// at their "no wait" maxima).  Through the builtin, not inline asm, so that hipcc's waitcnt pass
+// sees it and knows which loads it retired: after an asm wait hipcc still waited for them itself,
+// and while an LDS-DMA is in flight it does so with vmcnt(0).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 void set_error(const std::string& msg);
 
 // A/B switches and profiling ablations exist only in the profiling build (`make prof` ->

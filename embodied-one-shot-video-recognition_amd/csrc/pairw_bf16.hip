@@ -226,9 +226,9 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0) + 2 * G2 * NPT;
       constexpr int YOUNG_PRO = XS * NPT + (DSC ? 0 : 2 * RD * NPT);
       if (u == 0)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST) : "memory");
+        vm_wait<(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST)>();
       else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YOUNG) : "memory");
+        vm_wait<YOUNG>();
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       const int nch = ch + 1 < NCH ? ch + 1 : 0;  // the last chunk prefetches the next round's chunk 0
