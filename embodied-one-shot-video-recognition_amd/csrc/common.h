@@ -167,6 +167,7 @@ struct Pair1x1Args {
   // pairw_bf16 with the downsample (cds > 0): x2 is [N][H2][W2][cds], read at (2 oh, 2 ow) of
   // output pixel (n, oh, ow) of the Ho x Wo map
   int Ho, Wo, H2, W2;
+  int abl;  // profiling-build ablation bits (EOSV_CONV_ABL), 0 otherwise
 };
 bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);

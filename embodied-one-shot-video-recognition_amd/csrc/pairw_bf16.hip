@@ -87,9 +87,12 @@ struct PairW {
   static_assert(PPW < XS + 2 * G2, "DMA pieces go out one per fragment group, the residual loads after them");
 };
 
-template <int CMID, int CEXP, int C1, int NPT, int DSC>
+// ABL (profiling-only instance, EOSV_CONV_ABL bits; results wrong): 1 no weight DMA, 2 no
+// residual loads, 4 no Y stores, 8 no MFMAs, 16 no chunk barriers, 32 no Z stores, 64 no X loads
+template <int CMID, int CEXP, int C1, int NPT, int DSC, bool ABL = false>
 __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   using P = PairW<CMID, CEXP, C1, NPT, DSC>;
+  const int abl = ABL ? a.abl : 0;
   constexpr int K3 = P::K3, XSM = P::XSM;
   constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW, NT = 64 * P::NW;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS];
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
         vm_wait<(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST)>();
       else
         vm_wait<YOUNG>();
-      __builtin_amdgcn_s_barrier();
+      if (!(abl & 16)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       const int nch = ch + 1 < NCH ? ch + 1 : 0;  // the last chunk prefetches the next round's chunk 0
 
@@ -263,8 +266,8 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       bf16x8 yf[NPT][2];
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
-        if (gi < PPW) dma_piece(gi, nch, slot ^ 1);
-        if (!DSC && gi == PPW) {  // branch-free (scalar selects): a branch here made hipcc wait vmcnt(0) at the join
+        if (gi < PPW && !(abl & 1)) dma_piece(gi, nch, slot ^ 1);
+        if (!DSC && gi == PPW && !(abl & 2)) {  // branch-free (scalar selects): a branch here made hipcc wait vmcnt(0) at the join
           const bool here = ch + RD < NCH;
           RoundRes rr;
           rr.res = here ? cur.res : nxt.res;
@@ -275,7 +278,8 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
         // the next group's 4 LDS reads issue before this group's 4 MFMAs
         if (gi + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 4 * NPT, 0);
-        if (gi < XS) {  // GEMM1: chunk couts, tiles i = 0..3 of 16 permuted rows
+        if (abl & 8) {
+        } else if (gi < XS) {  // GEMM1: chunk couts, tiles i = 0..3 of 16 permuted rows
 #pragma unroll
           for (int t = 0; t < NPT; ++t) {
             const bf16x8 bx = __builtin_bit_cast(bf16x8, xf[t][gi]);
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
         __builtin_amdgcn_sched_barrier(0);
         if (gi == XS - 1) {
           if (u == 3 && cp + 4 == NCH) {  // the round's X is dead: the next round's goes into the same registers
-            load_x(nxt, rt + gridDim.x, xf);
+            if (!(abl & 64)) load_x(nxt, rt + gridDim.x, xf);
             __builtin_amdgcn_sched_barrier(0);
           }
           // epilogue 1: + shift, + residual, ReLU, bf16 -> Y (global) and the GEMM2 B fragments
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
                 }
                 pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
               }
-              __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2,
+              if (!(abl & 4)) __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2,
                                                      (ch * 64 + 32 * hh) * 2, 0);
               yf[t][hh] = __builtin_bit_cast(bf16x8, pk);
             }
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
             const float v1 = acc2[t][g][2 * hh + (e1 >> 2)][e1 & 3] + b1s[c0 + e1];
             pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
           }
-          __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, ((pw + 16 * t) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2, 0);
+          if (!(abl & 32)) __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, ((pw + 16 * t) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2, 0);
         }
     cur = nxt;
   }
@@ -360,6 +364,14 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   const long long nrounds = (a.M + PW_TILE - 1) / PW_TILE;
   if (a.plan) return record_launch(a.plan, nrounds, occ);
   const long long grid = std::min<long long>(nrounds, (long long)occ * device_cu_count());
+#ifdef EOSV_PROFILING
+  static const int abl = env_switch("EOSV_CONV_ABL", 0);
+  if (abl) {
+    Pair1x1Args b = a;
+    b.abl = abl;
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, true>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, b);
+  } else
+#endif
   hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
