@@ -14,10 +14,14 @@ namespace eosv {
 // at their "no wait" maxima).  Through the builtin, not inline asm, so that hipcc's waitcnt pass
 // sees it and knows which loads it retired: after an asm wait hipcc still waited for them itself,
 // and while an LDS-DMA is in flight it does so with vmcnt(0).
+// The empty asm after it is the compiler-level memory barrier the builtin is not: without it,
+// LDS reads of a ring slot could be scheduled above the wait (and the s_barrier after it) that
+// makes the slot's DMA complete -- a race (r03: wrong bf16 features one run in several).
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
 }
 
 void set_error(const std::string& msg);

@@ -233,6 +233,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       else
         vm_wait<YOUNG>();
       if (!(abl & 16)) __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");  // no LDS read of the slot moves above the barrier (s_barrier is not a compiler memory barrier)
       __builtin_amdgcn_sched_barrier(0);
       const int nch = ch + 1 < NCH ? ch + 1 : 0;  // the last chunk prefetches the next round's chunk 0
 
