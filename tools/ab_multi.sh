@@ -11,6 +11,8 @@ if [ -n "$CHECK" ]; then
     cp tools/ablib/libeosv_$v.so $LIB
     timeout -k 10 120 tests/native/conv_check > gpurun_out/ab_multi_check_$v.log 2>&1 || { grep -E "FAIL|failures" gpurun_out/ab_multi_check_$v.log | head; cp /tmp/libeosv_tree.so $LIB; exit 1; }
     echo "[$v] $(grep failures gpurun_out/ab_multi_check_$v.log)"
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_parity.py -k batch_invariance > gpurun_out/ab_multi_bi_$v.log 2>&1 || { tail -3 gpurun_out/ab_multi_bi_$v.log; cp /tmp/libeosv_tree.so $LIB; exit 1; }
+    echo "[$v] $(tail -1 gpurun_out/ab_multi_bi_$v.log)"
   done
 fi
 for pass in 1 2; do
