@@ -172,12 +172,15 @@ struct Pair1x1Args {
   // output pixel (n, oh, ow) of the Ho x Wo map
   int Ho, Wo, H2, W2;
   int abl;  // profiling-build ablation bits (EOSV_CONV_ABL), 0 otherwise
+  // pairw_bf16: elements each of x, res / y and z holds (it runs on whole PAIRW_TILE-pixel tiles)
+  long long cap_elems;
 };
 bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
 // pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
 // streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
-bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
+constexpr int PAIRW_TILE = 128;  // pixels per pairw round
+bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems);
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);

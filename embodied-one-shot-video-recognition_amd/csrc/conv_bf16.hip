@@ -42,36 +42,56 @@ __device__ __forceinline__ int tap_order(const ConvArgs& a, int t) {
   constexpr unsigned long long PERM9 = 0x453718620ull;  // t -> tap: 0 2 6 8 1 7 3 5 4
   return (a.stride == 2 && a.KH == 3 && a.KW == 3) ? (int)((PERM9 >> (4 * t)) & 15) : t;
 }
+// (tap, first channel) of the K-step starting at k0 in the stored K order: k0 is a multiple of
+// the kernel's BK (64 or 32); Cin is a multiple of 64, so a K-step never straddles a tap
+__device__ __forceinline__ void ktap(const ConvArgs& a, int k0, int& tap, int& c0) {
+  const int taps = a.KH * a.KW;
+  if (a.kcm) {  // K = (cin / 64, kh, kw, cin % 64)
+    const int chunk = k0 / (64 * taps);
+    const int kk = k0 - chunk * 64 * taps;
+    tap = tap_order(a, kk >> 6);
+    c0 = chunk * 64 + (kk & 63);
+  } else {
+    tap = k0 / a.Cin;
+    c0 = k0 - tap * a.Cin;
+    tap = tap_order(a, tap);
+  }
+}
 // weight column (the stored K order) of the K-step starting at k0 of the kernel's K loop
 __device__ __forceinline__ int wcol(const ConvArgs& a, int k0) {
   if (a.x2 && k0 >= a.K1) return k0;  // folded downsample columns
   const int taps = a.KH * a.KW;
   if (taps == 1) return k0;
-  if (a.kcm) {
-    const int chunk = k0 / (64 * taps);
-    return chunk * 64 * taps + tap_order(a, (k0 - chunk * 64 * taps) >> 6) * 64;
-  }
-  const int t = k0 / a.Cin;
-  return tap_order(a, t) * a.Cin + (k0 - t * a.Cin);
+  int tap, c0;
+  ktap(a, k0, tap, c0);
+  return a.kcm ? (c0 >> 6) * 64 * taps + tap * 64 + (c0 & 63) : tap * a.Cin + c0;
 }
 
-template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false>
+#ifndef EOSV_BF16_STAG
+#define EOSV_BF16_STAG 1
+#endif
+
+// BK: K per ring slot, 64 (128-B rows) or 32 (64-B rows: half the bytes per slot, so a 4-deep
+// ring -- three K-steps in flight -- fits where the 64-deep slots allowed two)
+template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false, int BK = 64>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
-  constexpr int BK = 64;  // bf16 elements per row = 128 B
+  static_assert(BK == 64 || (BK == 32 && !STEM && MF == 16), "BK 32: 16x16x32 MFMAs, no stem");
+  constexpr int CPR = BK / 8;    // 16-B chunks per LDS row
+  constexpr int RPP = 64 / CPR;  // rows per 1-KiB DMA piece (one wave-instruction)
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / MF;
   constexpr int TN = BN / WN / MF;
   constexpr int ACC = MF * MF / 64;  // f32 accumulator elements per lane per tile
-  constexpr int AI = BM / (8 * NW);
-  constexpr int BI = BN / (8 * NW);
+  constexpr int AI = BM / (RPP * NW);
+  constexpr int BI = BN / (RPP * NW);
   constexpr int STAGE = (BM + BN) * BK;  // bf16 elements per ring slot
   static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile shape");
-  static_assert(NS == 2 || NS == 3, "ring depth");
+  static_assert(NS >= 2 && NS <= 5, "ring depth");
   __shared__ __attribute__((aligned(16))) u16 smem[NS * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int HoWo = a.Ho * a.Wo;
   const int M = a.N * HoWo;
@@ -85,16 +105,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const u16* __restrict__ w = (const u16*)a.w;
   const u16* zero = (const u16*)a.zero;
 
-  const int lr = lane >> 3;
-  const int pc = lane & 7;
+  const int lr = lane / CPR;
+  const int pc = lane & (CPR - 1);
   const int xrow = ((a.W + 2 * a.pad + 1) & ~1) * 3;  // STEM: elements per padded input row
   const u16* arow[AI];
   const u16* arow2[DS ? AI : 1];  // DS: the fused downsample's input pixel (always in bounds)
   int aih[AI], aiw[AI], alc[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
-    const int row = wid * (BM / NW) + 8 * j + lr;
-    const int lc = pc ^ ((row >> 1) & 7);
+    const int row = wid * (BM / NW) + RPP * j + lr;
+    const int lc = pc ^ ((row >> 1) & (CPR - 1));
     alc[j] = lc;
     const int m = m0 + row;
     if (m < M) {
@@ -123,8 +143,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   const u16* brow[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
-    const int row = wid * (BN / NW) + 8 * j + lr;
-    const int lc = pc ^ ((row >> 1) & 7);
+    const int row = wid * (BN / NW) + RPP * j + lr;
+    const int lc = pc ^ ((row >> 1) & (CPR - 1));
     const int n = n0 + row;
     brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 8 : nullptr;
   }
@@ -137,7 +157,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < (DS ? AI : 1); ++j) {
         const u16* src = arow2[j] ? arow2[j] + (SPLIT ? split_chan(k0 - a.K1, a.Cin2) : k0 - a.K1) : zero;
-        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        u16* dst = As + (wid * (BM / NW) + RPP * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     } else if constexpr (STEM) {
@@ -147,21 +167,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         const int kh = g / 3;
         const bool ok = aih[j] > -(1 << 27) && kh < a.KH;
         const u16* src = ok ? arow[j] + kh * xrow + (g - 3 * kh) * 8 : zero;
-        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        u16* dst = As + (wid * (BM / NW) + RPP * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     } else {
       int tap, c0;
-      const int taps = a.KH * a.KW;
-      if (a.kcm) {  // K = (cin / 64, kh, kw, cin % 64)
-        const int chunk = k0 / (64 * taps);
-        tap = tap_order(a, (k0 - chunk * 64 * taps) >> 6);
-        c0 = chunk * 64;
-      } else {
-        tap = k0 / a.Cin;
-        c0 = k0 - tap * a.Cin;
-        tap = tap_order(a, tap);
-      }
+      ktap(a, k0, tap, c0);
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
       const long long toff = ((long long)kh * a.W + kw) * a.xs + (SPLIT ? split_chan(c0, a.Cin) : c0);
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         const int ih = aih[j] + kh, iw = aiw[j] + kw;
         const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const u16* src = ok ? arow[j] + toff : zero;
-        u16* dst = As + (wid * (BM / NW) + 8 * j) * BK;
+        u16* dst = As + (wid * (BM / NW) + RPP * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     }
@@ -179,7 +190,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
       const u16* src = brow[j] ? brow[j] + kb : zero;
-      u16* dst = Bs + (wid * (BN / NW) + 8 * j) * BK;
+      u16* dst = Bs + (wid * (BN / NW) + RPP * j) * BK;
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }
   };
@@ -196,25 +207,41 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // fragment lane map: row r = lane % MF, 16-B chunk q = lane / MF of the MFMA's k-slice
   const int r = lane & (MF - 1);
   const int q = lane / MF;
-  const int sw = (r >> 1) & 7;  // tile bases are multiples of 16 rows: the swizzle depends on r only
+  const int sw = (r >> 1) & (CPR - 1);  // tile bases are multiples of 16 rows: the swizzle depends on r only
   const int nk = (EOSV_ABL(a) & 1024) ? 0 : a.K / BK;  // 1024 (profiling-only): no K-loop
-  // NS-deep ring: NS-1 stages in flight; with NS = 3 the wait before each barrier is a
-  // counted vmcnt (the newest stage stays in flight across it) and barriers are raw
-  // s_barrier (__syncthreads would drain it with vmcnt(0))
+  // NS-deep ring: NS-1 stages in flight; the wait before each barrier is a counted vmcnt (the
+  // newer stages stay in flight across it) and barriers are raw s_barrier (__syncthreads would
+  // drain them with vmcnt(0)).  wait_stages(n): all but the wave's n newest stages have landed.
   constexpr int PER = AI + BI;  // DMA instructions per stage per wave
+  auto wait_stages = [&](int n) {
+    if (NS >= 5 && n >= 3)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * PER) : "memory");
+    else if (NS >= 4 && n >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PER) : "memory");
+    else if (NS >= 3 && n >= 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
   for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p, 0);
-  if (NS == 3 && nk > 1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wait_stages(min(NS - 2, nk - 1));
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
   int cur = 0, wslot = NS - 1;
+  // The two waves of a SIMD are w and w + NW/2.  EOSV_BF16_STAG bit 0 (default): the upper half
+  // issues its DMA in the middle of the K-step (after half of its MFMA groups) instead of at its
+  // start, so that each SIMD pairs one wave's DMA issue with the other's MFMAs (r03, R50 bf16 per
+  // 3200 frames: 3x3 convs 4-7 % faster, 1x1s unchanged, the 1x1 + folded-downsample convs 6-8 %
+  // slower, so those keep the plain order unless bit 2); bit 1: s_setprio 1 for the upper half
+  // (measured slower).
+  const bool late = (EOSV_BF16_STAG & 1) && MF == 16 && (!DS || a.KH > 1 || (EOSV_BF16_STAG & 4)) && wid >= NW / 2;
+  if ((EOSV_BF16_STAG & 2) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (int kt = 0; kt < nk; ++kt) {
     const bool issue = kt + NS - 1 < nk;
     // EOSV_ABL(a) (profiling-only ablations, results wrong when set): 1 no main-loop loads,
     // 4 no A loads, 8 no B loads, 16 no ds_reads, 32 no MFMAs, 64 no epilogue
-    if (issue && !(EOSV_ABL(a) & 1)) stage((kt + NS - 1) * BK, wslot, EOSV_ABL(a));
+    if (issue && !late && !(EOSV_ABL(a) & 1)) stage((kt + NS - 1) * BK, wslot, EOSV_ABL(a));
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + BM * BK;
     constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
@@ -261,6 +288,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[g & 1], bfr[s & 1][j], acc[i][j], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
+          if (late && issue && g == NG / 2 - 1 && !(EOSV_ABL(a) & 1)) {
+            stage((kt + NS - 1) * BK, wslot, EOSV_ABL(a));
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
     } else
@@ -293,12 +324,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (NS == 3 && issue)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage kt + 1 must have landed; the ones issued after it (up to kt + NS - 1) may fly on
+    wait_stages(min(NS - 2, nk - 2 - kt));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     cur = cur + 1 == NS ? 0 : cur + 1;
     wslot = wslot + 1 == NS ? 0 : wslot + 1;
   }
@@ -429,37 +459,46 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   }
 }
 
+// Ring shape of the 256x256 / 512x128 im2col tiles: 0 = 64-deep K-steps in a 2-slot ring;
+// bit 0 (256x256) / bit 2 (512x128): 32-deep K-steps in a 4-slot ring; bit 1: 256x256 in 5 slots.
+// r03 A/B (R50 bf16, ms per 3200 frames): the 32-deep rings are 12-20 % slower on every 3x3 conv
+// (0.63 -> 0.74-0.80), whatever the depth: two or three K-steps in flight do not pay for the
+// 64-B rows (twice the row segments per staged byte); kept as a build option only.
+#ifndef EOSV_BF16_K32
+#define EOSV_BF16_K32 0
+#endif
+
 static int bf16_rows() {
   static int v = env_switch("EOSV_BF16_ROWS", 1);  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, bool STEM, int NS = 2>
+template <int BM, int BN, int WM, int WN, bool STEM, int NS = 2, int BK = 64>
 static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
   if (a.plan) {
     static const int occ =
-        kernel_occupancy((const void*)conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false>, 64 * WM * WN);
+        kernel_occupancy((const void*)conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, false, BK>, 64 * WM * WN);
     return record_launch(a.plan, nb, occ);
   }
   if (a.split) {
     if (STEM || (a.x2 && (a.K1 % 64 || a.Cin2 % 64)))
       return set_error("conv_bf16: split layout shape"), EOSV_ERR_UNSUPPORTED;
     if (a.x2)
-      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, true>), dim3((unsigned)nb),
+      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, true, BK>), dim3((unsigned)nb),
                          dim3(64 * WM * WN), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, true>), dim3((unsigned)nb),
+      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, true, BK>), dim3((unsigned)nb),
                          dim3(64 * WM * WN), 0, s, a);
   } else if (a.x2) {
     if (STEM || a.K1 % 64 || a.Cin2 % 64) return set_error("conv_bf16: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
-                       s, a);
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, false, BK>), dim3((unsigned)nb),
+                       dim3(64 * WM * WN), 0, s, a);
   } else {
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS, false>), dim3((unsigned)nb), dim3(64 * WM * WN), 0,
-                       s, a);
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS, false, false, BK>), dim3((unsigned)nb),
+                       dim3(64 * WM * WN), 0, s, a);
   }
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
@@ -505,8 +544,15 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return launch_bf16<256, 128, 2, 2, false>(a, s);
   }
 #endif
-  if (a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
-  if (a.Cout >= 256) return launch_bf16<256, 256, 2, 4, false>(a, s);
+  if (a.Cout == 128) {
+    if constexpr ((EOSV_BF16_K32 & 4) != 0) return launch_bf16<512, 128, 4, 2, false, 4, 32>(a, s);
+    return launch_bf16<512, 128, 4, 2, false>(a, s);
+  }
+  if (a.Cout >= 256) {
+    if constexpr ((EOSV_BF16_K32 & 1) != 0) return launch_bf16<256, 256, 2, 4, false, 4, 32>(a, s);
+    if constexpr ((EOSV_BF16_K32 & 2) != 0) return launch_bf16<256, 256, 2, 4, false, 5, 32>(a, s);
+    return launch_bf16<256, 256, 2, 4, false>(a, s);
+  }
   return launch_bf16<128, 64, 2, 2, false>(a, s);
 }
 

@@ -21,8 +21,8 @@
 // (+ residual) + ReLU, 8-B stores; no LDS staging, no epilogue barriers.
 //
 // Pipeline per strip: issue next strip's DMA (buffer cur^1) and this strip's residual loads
-// -> MFMAs on buffer cur -> epilogue (exactly 8 global stores per lane, younger than the
-// DMA) -> vmcnt(8) + barrier.
+// -> MFMAs on buffer cur -> vmcnt(0) (the DMA, issued a strip earlier) -> epilogue (8 global
+// stores per lane, left in flight) -> barrier.
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -210,11 +210,11 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
 
     // Epilogue straight from registers: per (pixel tile, cout tile) a lane owns 4 adjacent
     // channels of one pixel -> one 8-B store (16 lanes x 32 B per pixel row per instruction).
-    if (res) {
-      // the asm loads above (and the prefetch DMA, issued before them) have landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
-    }
+    // the prefetch DMA (and the asm residual loads above) have landed: waited for here, before
+    // the stores, and not by a count of younger stores after them -- vmcnt retires a store ahead
+    // of an older load, so a counted wait past stores does not cover the DMA (r03, pairw_bf16)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -235,10 +235,8 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
         const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
         if (!(abl & 64)) *(uint2*)(y + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q) = make_uint2(lo, hi);
       }
-    if (abl & 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // next strip's DMA (issued before this strip's 8 stores per lane) must have landed, and
-    // every wave's reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // every wave's next-strip DMA has landed (its wait above) and its reads of buffer cur are done
+    // (lgkmcnt(0) ends the k-loop) before buffer cur is refilled; the stores stay in flight
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -191,10 +191,10 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
       __builtin_amdgcn_sched_barrier(0);
     });
 
-    if constexpr (RES) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's residual DMA (and the prefetch) landed
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    // this wave's residual DMA and next-strip prefetch have landed: waited for before the stores,
+    // not by a count of younger stores after them (vmcnt retires a store ahead of an older load)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < TILES; ++i) {
       f32x4 rv = {0.f, 0.f, 0.f, 0.f};
@@ -212,13 +212,8 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
       // rewritten, which only the compiler's hazard recognizer inserts
       *(f32x4*)dst = v;
     }
-    // the next strip's DMA (issued before this strip's stores) has landed, and every wave's
-    // reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
-    if (abl & 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (TILES == 7)
-      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // every wave's next-strip DMA has landed (the wait above) and its reads of buffer cur are
+    // done (lgkmcnt(0) ends the k-loop) before it is refilled; the stores stay in flight
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
   }

@@ -202,10 +202,10 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    if constexpr (RES) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // residual (and the prefetch, older) landed
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    // residual and next-strip prefetch landed: waited for before the stores, not by a count of
+    // younger stores after them (vmcnt retires a store ahead of an older load)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < TILES; ++i) {
       float v[4];
@@ -231,10 +231,8 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
       asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(hv) : "memory");
       asm volatile("global_store_dwordx2 %0, %1, off offset:128" ::"v"(dst), "v"(lv) : "memory");
     }
-    // the next strip's DMA (issued before this strip's 14 stores) has landed, and every wave's
-    // reads of buffer cur are done (lgkmcnt(0) ends the k-loop) before it is refilled
-    if (abl & 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+    // every wave's next-strip DMA has landed (the wait above) and its reads of buffer cur are
+    // done (lgkmcnt(0) ends the k-loop) before it is refilled; the stores stay in flight
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
   }

@@ -488,6 +488,12 @@ static bool pairw_enabled() {
   return v;
 }
 
+// elements every activation buffer holds (the sub-chunk scratch, when on, is the smaller one)
+static long long act_buffer_elems(const eosv_handle* h) {
+  const long long f = h->sub_frames > 0 ? std::min(h->sub_frames, h->d.max_frames) : h->d.max_frames;
+  return f * (long long)h->act_elems;
+}
+
 static bool pair_ok(const eosv_handle* h, const Block& b, const Block* nb, long long M) {
   if (!pair_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || !nb || !nb->bottleneck) return false;
   const Conv &c3 = b.c3, &n1 = nb->c1;
@@ -497,7 +503,7 @@ static bool pair_ok(const eosv_handle* h, const Block& b, const Block* nb, long 
     // stride 2), or a plain residual block
     const bool ds = b.has_ds && b.fuse_ds && b.ds.stride == 2 && b.c2.stride == 2;
     if (!pairw_enabled() || (b.has_ds && !ds)) return false;
-    return pairw_bf16_ok(c3.cin, c3.cout, n1.cout, ds ? c3.kds : 0, M);
+    return pairw_bf16_ok(c3.cin, c3.cout, n1.cout, ds ? c3.kds : 0, M, act_buffer_elems(h));
   }
   if (b.c2.stride != 1 || (b.has_ds && !(b.fuse_ds && b.ds.stride == 1))) return false;
   return pair1x1_bf16_ok(c3.cin, c3.cout, n1.cout, b.has_ds ? c3.kds : 0, M);
@@ -526,6 +532,7 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
   p.Wo = wo;
   p.H2 = hin;
   p.W2 = win;
+  p.cap_elems = act_buffer_elems(h);
   const bool wide = p.cmid != 64;
   const double flops = 2.0 * M * ((double)b.c3.cout * (b.c3.cin + p.cds) + (double)nb.c1.cout * nb.c1.cin);
   if (h->planning) {

@@ -25,9 +25,9 @@
 // K is walked in the unfused kernels' order (32-wide slices, increasing k), bias then residual
 // then ReLU then round-to-nearest bf16: both maps equal the unfused conv3 -> conv1 pair's bit for
 // bit (tests/native/conv_check.cpp).  The residual of chunk ch + 3 is loaded while chunk ch
-// computes, the next round's X during the round's last chunk; loads / stores use buffer resources based at the round's first
-// pixel, so tail pixels (M % 128) read zeros and their stores are dropped, without a branch; their
-// per-lane part is the VGPR offset, the chunk / channel-group part the scalar offset.
+// computes, the next round's X during the round's last chunk; loads / stores use buffer resources
+// based at the round's first pixel (per-lane part the VGPR offset, chunk / channel-group part the
+// scalar offset), over whole 128-pixel tiles: the tail round runs on the buffers' padding.
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -57,7 +57,7 @@ __device__ __forceinline__ void dma16(const unsigned char* src, void* lds) {
 }
 }  // namespace
 
-constexpr int PW_TILE = 128;  // pixels per round
+constexpr int PW_TILE = PAIRW_TILE;  // pixels per round
 
 // NPT: 16-pixel tiles per wave.  NPT = 1: 8 waves (two per SIMD); NPT = 2: 4 waves (one per SIMD,
 // 512 VGPRs) that read each LDS weight fragment once for 32 pixels -- the LDS feeds one fragment per
@@ -138,14 +138,22 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       dma16((const unsigned char*)(a.b3 + ch * 64) + lane * 16, smem + slot * P::STAGE + P::STAGE_W);
   };
 
-  // ---- per-round resources (based at the round's first pixel; tails read 0, stores dropped)
+  // ---- per-round resources, based at the round's first pixel and always a whole 128-pixel tile:
+  // the tail round (M % 128) reads and writes its padding pixels p >= M like any others (garbage
+  // in, garbage out, never read: every output pixel depends on its own input pixel only; the
+  // launcher checks that the buffers hold the padded tile).  Masking them instead, with buffer
+  // records ending at M, made the tail round's loads / stores partly out of range, and the tail
+  // round's features then changed from run to run (r03, tools/race_probe.py).  A round past the
+  // last one (the final round's prefetch) gets empty records: its loads return 0 without touching
+  // memory.  (Re-reading the last round there instead -- lines another workgroup is rewriting in
+  // place, y = res -- made features of other frames change from run to run in later launches.)
   struct RoundRes {
     __amdgpu_buffer_rsrc_t x, res, y, z;
   };
   auto round_res = [&](long long t) {
     RoundRes rr;
     const long long p0 = t * PW_TILE;
-    const long long n = t < nrounds ? (M - p0 < PW_TILE ? M - p0 : PW_TILE) : 0;
+    const long long n = t < nrounds ? PW_TILE : 0;
     rr.x = rsrc((const unsigned short*)a.x + p0 * CMID, n * CMID * 2);
     rr.res = rsrc((const unsigned short*)a.res + p0 * CEXP, n * CEXP * 2);
     rr.y = rsrc((unsigned short*)a.y + p0 * CEXP, n * CEXP * 2);
@@ -219,14 +227,20 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       // This wave's DMA of chunk ch is done, then every wave's (barrier): the slot is complete,
       // and slot ^ 1 (chunk ch - 1) is free for the next chunk's DMA.  In chunk ch - 1 the DMA
       // pieces went out with its first PPW fragment groups (one per group: an LDS-DMA issue costs
-      // the wave ~60-185 cycles, so all of them at once idled the SIMD's MFMA pipe); the VMEM ops
+      // the wave ~60-185 cycles, so all of them at once idled the SIMD's MFMA pipe); the loads
       // issued after the last piece (order pinned by the sched_barriers) may stay in flight:
-      // 2 NPT residual loads (group PPW), the 2 NPT Y stores and, in the round's last chunk, the
-      // next round's XS NPT X loads when the epilogue (after group XS - 1) follows the last piece,
-      // and the last chunk's 2 G2 NPT Z stores; before the loop: XS NPT X loads + 2 RD NPT residual
-      // loads after the pieces.
-      constexpr int YOUNG = NRES + (XS >= PPW ? 2 * NPT : 0);
-      constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0) + 2 * G2 * NPT;
+      // 2 NPT residual loads (group PPW) and, in the round's last chunk, the next round's XS NPT
+      // X loads when the epilogue (after group XS - 1) follows the last piece; before the loop:
+      // XS NPT X loads + 2 RD NPT residual loads after the pieces.  Only loads are counted: vmcnt
+      // retires loads (the DMA included) in order among themselves, but a store can retire ahead
+      // of an older load, so counting the Y / Z stores issued after the last piece as still in
+      // flight let a wave pass with a piece not landed (r03: features of a round changed from run
+      // to run, mostly the tail round's; tools/race_probe.py, conv_check's repeated pairs).  A
+      // store still in flight here only makes the wait stricter (measured: stage-2 pairs 1.43 ->
+      // 1.55 ms, stage-3 0.81 -> 0.87 per 3200 frames; deferring the Y stores by a chunk, to have
+      // them retired by then, gave wrong results and was dropped).
+      constexpr int YOUNG = NRES;
+      constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0);
       constexpr int YOUNG_PRO = XS * NPT + (DSC ? 0 : 2 * RD * NPT);
       if (u == 0)
         vm_wait<(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST)>();
@@ -305,7 +319,6 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
           // epilogue 1: + shift, + residual, ReLU, bf16 -> Y (global) and the GEMM2 B fragments
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-            const int c0 = ch * 64 + 32 * hh + 8 * q;
             // read as the fragments are (bf16x8 through the slot pointer): a float4 read here got a
             // vmcnt(0) from hipcc, as if it could alias the DMA in flight
             const unsigned char* b3c = ws + P::STAGE_W + (32 * hh + 8 * q) * 4;
@@ -327,8 +340,8 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
                 }
                 pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
               }
-              if (!(abl & 4)) __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2,
-                                                     (ch * 64 + 32 * hh) * 2, 0);
+              if (!(abl & 4))
+                __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2, (ch * 64 + 32 * hh) * 2, 0);
               yf[t][hh] = __builtin_bit_cast(bf16x8, pk);
             }
           }
@@ -378,14 +391,17 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   return EOSV_OK;
 }
 
-bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M) {
+bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems) {
   if (M <= 0) return false;
+  // the tail round reads and writes whole tiles: x, res / y and z must hold the padded pixel count
+  const long long padded = (M + PW_TILE - 1) / PW_TILE * PW_TILE;
+  if (padded * std::max(cmid, std::max(cexp, c1)) > cap_elems) return false;
   if (cds) return cmid == 128 && cexp == 512 && c1 == 128 && cds == 256;  // stage-2 block 0
   return (cmid == 128 && cexp == 512 && (c1 == 128 || c1 == 256)) || (cmid == 256 && cexp == 1024 && c1 == 256);
 }
 
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
-  if (!pairw_bf16_ok(a.cmid, a.cexp, a.c1, a.cds, a.M) || !a.x || !a.w3 || !a.b3 || !a.w1 || !a.b1 || !a.y || !a.z ||
+  if (!pairw_bf16_ok(a.cmid, a.cexp, a.c1, a.cds, a.M, a.cap_elems) || !a.x || !a.w3 || !a.b3 || !a.w1 || !a.b1 || !a.y || !a.z ||
       (a.cds ? (!a.x2 || a.res || a.Ho <= 0 || a.Wo <= 0 || a.H2 < 2 * a.Ho - 1 || a.W2 < 2 * a.Wo - 1) : (!a.res || a.x2)))
     return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   if (a.cds) return launch_pairw<128, 512, 128, 1, 256>(a, s);

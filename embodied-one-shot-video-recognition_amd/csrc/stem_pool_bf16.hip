@@ -274,6 +274,10 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
     stem_row(2 * py, a1);
     stem_row(2 * py + 1, a2);
     const bool ok1 = colok && 2 * py < Hs, ok2 = colok && 2 * py + 1 < Hs;
+    // !DIRECT: the next step's rows (staged at this step's start) have landed before this step's
+    // stores go out -- not counted past them: vmcnt retires a store ahead of an older load, and
+    // a wave with no writer lanes issues no stores at all
+    if constexpr (!DIRECT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned pk4[4][2];  // pooled bf16 pairs, stored after the DIRECT conversion
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -313,9 +317,9 @@ __global__ __launch_bounds__(64 * MAX_TILES) void stem_pool_bf16_kernel(const u1
         if (writer) *(uint2*)(yimg + ((long long)py * Wq + px) * 64 + j * 16 + 4 * q) = make_uint2(pk4[j][0], pk4[j][1]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
-      // next step's rows have landed (their DMA is older than this step's 4 stores) and every
-      // wave is done reading the slots the step after will overwrite
-      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      // every wave's next-step rows have landed (the wait above) and it is done reading the
+      // slots the step after will overwrite
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
   }

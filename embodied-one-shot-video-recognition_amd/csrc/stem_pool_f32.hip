@@ -258,6 +258,10 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
         v[k][e] = fmaxf(fmaxf(prev[k][e], ok1 && colok[k] ? a1[k][e] : NEG), v2);  // row max
         prev[k][e] = v2;
       }
+    // the next step's rows (staged at this step's start) have landed: waited for before the
+    // stores, not by a count of younger stores after them (vmcnt retires a store ahead of an
+    // older load, and a store whose lanes are all past the map may not be issued at all)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
       const int px = 8 * k + (r16 >> 1);
@@ -289,12 +293,9 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
         *(float4*)(yimg + ((long long)py * Wq + px) * 64 + 16 * g + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
-    // next step's rows have landed (their DMA is older than this step's stores) and every
-    // wave is done reading the slots the step after will overwrite
-    if constexpr (SPLIT)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * NT) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(NT) : "memory");
+    // every wave's next-step rows have landed (the wait above) and it is done reading the slots
+    // the step after will overwrite; the stores stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -507,7 +507,9 @@ static int check_pair(int N, int H, int W, int c1, bool ds) {
 
 // wide bottleneck pair (pairw_bf16.hip, stages 2-3) vs the unfused conv3 (1x1 cmid -> cexp +
 // residual) -> conv1 (1x1 cexp -> c1) through launch_conv_bf16: both maps bit-identical.  M
-// need not be a multiple of the 128-pixel round (tail pixels read zeros, their stores dropped).
+// need not be a multiple of the 128-pixel round: the tail round runs on the buffers' padding
+// (filled with NaN here: no valid output may depend on it), and it is repeated REPS times (its
+// results changed from run to run while it masked the padding with out-of-range buffer ops).
 static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds = 0) {
   // cds > 0: block 0 of a stage, conv3 + the folded stride-2 downsample reading x2 [N][2H][2W][cds]
   // (ragged: 2H - 1 when odd sizes are asked for through H2/W2 below), no residual
@@ -518,9 +520,16 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   auto fill = [&](std::vector<unsigned short>& v, float scale) {
     for (auto& e : v) e = f2bf(frand(s) * scale);
   };
-  std::vector<unsigned short> x(M * cmid), res(M * cexp), w3((size_t)cexp * K3), w1((size_t)c1 * cexp);
+  const long long Mp = (M + PAIRW_TILE - 1) / PAIRW_TILE * PAIRW_TILE;  // padded to whole rounds
+  std::vector<unsigned short> x(Mp * cmid, 0x7fc0), res(Mp * cexp, 0x7fc0), w3((size_t)cexp * K3), w1((size_t)c1 * cexp);
   std::vector<unsigned short> x2(cds ? (size_t)N * H2 * W2 * cds : 1);
-  fill(x, 1.f); fill(res, 1.f); fill(w3, 0.125f); fill(w1, 0.0625f); fill(x2, 1.f);
+  {
+    std::vector<unsigned short> xv(M * cmid), rv(M * cexp);
+    fill(xv, 1.f); fill(rv, 1.f);
+    std::copy(xv.begin(), xv.end(), x.begin());
+    std::copy(rv.begin(), rv.end(), res.begin());
+  }
+  fill(w3, 0.125f); fill(w1, 0.0625f); fill(x2, 1.f);
   std::vector<float> b3(cexp), b1(c1);
   for (auto& v : b3) v = frand(s) * 0.5f;
   for (auto& v : b1) v = frand(s) * 0.5f;
@@ -529,8 +538,7 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   void *dw3 = up(w3.data(), w3.size() * 2), *dw1 = up(w1.data(), w1.size() * 2);
   float *db3 = (float*)up(b3.data(), b3.size() * 4), *db1 = (float*)up(b1.data(), b1.size() * 4);
   void *y0, *z0, *y1, *z1, *dz;
-  hipMalloc(&y0, M * cexp * 2); hipMalloc(&y1, M * cexp * 2); hipMalloc(&z0, M * c1 * 2); hipMalloc(&z1, M * c1 * 2);
-  hipMemset(y1, 0xff, M * cexp * 2); hipMemset(z1, 0xff, M * c1 * 2);
+  hipMalloc(&y0, M * cexp * 2); hipMalloc(&y1, Mp * cexp * 2); hipMalloc(&z0, M * c1 * 2); hipMalloc(&z1, Mp * c1 * 2);
   hipMalloc(&dz, 256); hipMemset(dz, 0, 256);
   ConvArgs a{};
   a.x = dx; a.w = dw3; a.bias = db3; a.res = cds ? nullptr : dr; a.y = y0;
@@ -547,17 +555,25 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   p.x = dx; p.res = cds ? nullptr : dr; p.w3 = dw3; p.b3 = db3; p.w1 = dw1; p.b1 = db1;
   p.y = y1; p.z = z1; p.M = M; p.c1 = c1; p.cmid = cmid; p.cexp = cexp;
   if (cds) { p.x2 = dx2; p.cds = cds; p.Ho = H; p.Wo = W; p.H2 = H2; p.W2 = W2; }
-  const int rcp = launch_pairw_bf16(p, 0);
-  hipDeviceSynchronize();
+  p.cap_elems = Mp * std::max(cmid, std::max(cexp, c1));
   std::vector<unsigned short> hy0(M * cexp), hy1(M * cexp), hz0(M * c1), hz1(M * c1);
-  hipMemcpy(hy0.data(), y0, M * cexp * 2, hipMemcpyDeviceToHost); hipMemcpy(hy1.data(), y1, M * cexp * 2, hipMemcpyDeviceToHost);
-  hipMemcpy(hz0.data(), z0, M * c1 * 2, hipMemcpyDeviceToHost); hipMemcpy(hz1.data(), z1, M * c1 * 2, hipMemcpyDeviceToHost);
+  hipMemcpy(hy0.data(), y0, M * cexp * 2, hipMemcpyDeviceToHost);
+  hipMemcpy(hz0.data(), z0, M * c1 * 2, hipMemcpyDeviceToHost);
   long bady = 0, badz = 0;
   double maxd = 0;
-  for (size_t i = 0; i < hy0.size(); ++i)
-    if (hy0[i] != hy1[i]) ++bady, maxd = std::max(maxd, (double)fabs(bf2f(hy0[i]) - bf2f(hy1[i])));
-  for (size_t i = 0; i < hz0.size(); ++i)
-    if (hz0[i] != hz1[i]) ++badz, maxd = std::max(maxd, (double)fabs(bf2f(hz0[i]) - bf2f(hz1[i])));
+  int rcp = 0;
+  const int REPS = M % PAIRW_TILE ? 8 : 1;
+  for (int rep = 0; rep < REPS; ++rep) {
+    hipMemset(y1, 0xff, Mp * cexp * 2); hipMemset(z1, 0xff, Mp * c1 * 2);
+    rcp |= launch_pairw_bf16(p, 0);
+    hipDeviceSynchronize();
+    hipMemcpy(hy1.data(), y1, M * cexp * 2, hipMemcpyDeviceToHost);
+    hipMemcpy(hz1.data(), z1, M * c1 * 2, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < hy0.size(); ++i)
+      if (hy0[i] != hy1[i]) ++bady, maxd = std::max(maxd, (double)fabs(bf2f(hy0[i]) - bf2f(hy1[i])));
+    for (size_t i = 0; i < hz0.size(); ++i)
+      if (hz0[i] != hz1[i]) ++badz, maxd = std::max(maxd, (double)fabs(bf2f(hz0[i]) - bf2f(hz1[i])));
+  }
   double maxerr = 0;  // the unfused conv3 itself against double on the bf16 operands (a few pixels)
   for (long long m = 0; m < M; m += M / 7 + 1)
     for (int o = 0; o < cexp; o += 7) {
