@@ -36,6 +36,10 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
 }
 }  // namespace
 
+#ifndef EOSV_TS_STAG
+#define EOSV_TS_STAG 1
+#endif
+
 template <int BM, int BN, int WM, int WN, bool SPLIT>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) {
   constexpr int BK = 32;                        // channels per stage
@@ -170,17 +174,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   }
 
   const int nst = nst3 + (x2 ? a.Cin2 / BK : 0);
+  // EOSV_TS_STAG k > 0: the upper half of the waves (the partners w + NW/2 of a SIMD's pairs)
+  // issues its next-stage DMA after tap kw = k - 1 instead of at the stage's start (as
+  // conv_bf16_kernel's stagger: one wave's DMA issue beside the other's MFMAs).  r03, R50 bf16
+  // stage-2 3x3s per 3200 frames: k = 1 0.81-0.86 -> 0.77-0.82 ms (4-5 %), k = 2 1-2 %.
+  const int lkw = (EOSV_TS_STAG > 0 && wid >= NW / 2) ? EOSV_TS_STAG - 1 : -1;
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
   for (int st = 0; st < nst; ++st) {
     const int cur = st & 1;
-    if (st + 1 < nst) stage(st + 1, cur ^ 1);
+    if (st + 1 < nst && lkw < 0) stage(st + 1, cur ^ 1);
     const u16* As = smem + cur * STAGE;
     const u16* Bs = As + AR * BK;
     const bool ds = st >= nst3;  // a DS stage is read at offset 1 only (no taps, no edges)
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
+      if (kw > 0 && kw - 1 == lkw && st + 1 < nst) stage(st + 1, cur ^ 1);
       if (ds && kw != 1) continue;
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
@@ -203,6 +214,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
 
   // Epilogue as conv_bf16_kernel's (LDS-staged 16-B rows, buffer resources, branch-free)
