@@ -130,7 +130,11 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = a.bias ? *(const f32x4*)(a.bias + j * 16 + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int strip = blockIdx.x;
+  // strips dealt XCD-contiguously (as conv_rows_f32): at each step the 32 workgroups of an XCD
+  // walk 32 consecutive strips, so the 2 halo rows a strip shares with its neighbour are read
+  // from that XCD's L2 instead of another XCD's (round-robin placement put neighbours on
+  // different XCDs)
+  int strip = xcd_tile(blockIdx.x, gridDim.x, 1);
   if (strip < nstrips) stage(strip, 0);
   // vmcnt(0) as the builtin (not asm) so the compiler's wait tracking knows the bias loads
   // have landed and does not re-wait for them (draining the in-flight DMA) inside the loop
