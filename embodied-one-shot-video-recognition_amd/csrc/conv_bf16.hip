@@ -72,8 +72,11 @@ __device__ __forceinline__ int wcol(const ConvArgs& a, int k0) {
 #endif
 
 // BK: K per ring slot, 64 (128-B rows) or 32 (64-B rows: half the bytes per slot, so a 4-deep
-// ring -- three K-steps in flight -- fits where the 64-deep slots allowed two)
-template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false, int BK = 64>
+// ring -- three K-steps in flight -- fits where the 64-deep slots allowed two).
+// NSA > 0: separate rings, NSA slots for A (the im2col rows, loaded two K-steps ahead) and NS for
+// B (the weights, one K-step ahead; every workgroup reads the same weights, so they come from L2)
+template <int BM, int BN, int WM, int WN, bool STEM, int MF, int NS, bool DS, bool SPLIT = false, int BK = 64,
+          int NSA = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   static_assert(BK == 64 || (BK == 32 && !STEM && MF == 16), "BK 32: 16x16x32 MFMAs, no stem");
   constexpr int CPR = BK / 8;    // 16-B chunks per LDS row
@@ -87,7 +90,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   constexpr int STAGE = (BM + BN) * BK;  // bf16 elements per ring slot
   static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile shape");
   static_assert(NS >= 2 && NS <= 5, "ring depth");
-  __shared__ __attribute__((aligned(16))) u16 smem[NS * STAGE];
+  static_assert(NSA == 0 || (NSA == 3 && NS == 2 && !STEM), "split rings: 3 A slots, 2 B slots");
+  constexpr int SMEM = NSA ? NSA * BM * BK + NS * BN * BK : NS * STAGE;
+  __shared__ __attribute__((aligned(16))) u16 smem[SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -149,9 +154,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 8 : nullptr;
   }
 
-  auto stage = [&](int k0, int slot, int skip) {
-    u16* As = smem + slot * STAGE;
-    u16* Bs = As + BM * BK;
+  // A into A slot aslot, B into B slot bslot (one ring: both the same slot); skip 4: no A, 8: no B
+  auto stage = [&](int k0, int aslot, int bslot, int skip) {
+    u16* As = NSA ? smem + aslot * BM * BK : smem + aslot * STAGE;
+    u16* Bs = NSA ? smem + NSA * BM * BK + bslot * BN * BK : smem + bslot * STAGE + BM * BK;
     if (skip & 4) {
     } else if (DS && k0 >= a.K1) {
 #pragma unroll
@@ -223,8 +229,21 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p, 0);
-  wait_stages(min(NS - 2, nk - 1));
+  if constexpr (NSA > 0) {  // B(0), A(0), A(1); A(1) may stay in flight
+    if (nk > 0) {
+      stage(0, 0, 0, 4);
+      stage(0, 0, 0, 8);
+    }
+    if (nk > 1) {
+      stage(BK, 1, 0, 8);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(AI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+    for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p * BK, p, p, 0);
+    wait_stages(min(NS - 2, nk - 1));
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
@@ -237,13 +256,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // (measured slower).
   const bool late = (EOSV_BF16_STAG & 1) && MF == 16 && (!DS || a.KH > 1 || (EOSV_BF16_STAG & 4)) && wid >= NW / 2;
   if ((EOSV_BF16_STAG & 2) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // the K-step's DMA: one ring: stage kt + NS - 1 into slot wslot; split rings: B(kt + 1) then
+  // A(kt + 2) (in this order: the end-of-step wait leaves only A(kt + 2) in flight)
+  auto issue_step = [&](int kt) {
+    if (EOSV_ABL(a) & 1) return;
+    if constexpr (NSA > 0) {
+      if (kt + 1 < nk) stage((kt + 1) * BK, 0, (kt + 1) & 1, 4 | EOSV_ABL(a));
+      if (kt + 2 < nk) stage((kt + 2) * BK, (kt + 2) % NSA, 0, 8 | EOSV_ABL(a));
+    } else if (kt + NS - 1 < nk) {
+      stage((kt + NS - 1) * BK, wslot, wslot, EOSV_ABL(a));
+    }
+  };
   for (int kt = 0; kt < nk; ++kt) {
-    const bool issue = kt + NS - 1 < nk;
     // EOSV_ABL(a) (profiling-only ablations, results wrong when set): 1 no main-loop loads,
     // 4 no A loads, 8 no B loads, 16 no ds_reads, 32 no MFMAs, 64 no epilogue
-    if (issue && !late && !(EOSV_ABL(a) & 1)) stage((kt + NS - 1) * BK, wslot, EOSV_ABL(a));
-    const u16* As = smem + cur * STAGE;
-    const u16* Bs = As + BM * BK;
+    if (!late) issue_step(kt);
+    const u16* As = NSA ? smem + (kt % (NSA ? NSA : 1)) * BM * BK : smem + cur * STAGE;
+    const u16* Bs = NSA ? smem + NSA * BM * BK + (kt & 1) * BN * BK : As + BM * BK;
     constexpr int KS = MF == 32 ? 16 : 32;  // k per MFMA
     if constexpr (MF == 16) {
       if (!(EOSV_ABL(a) & (16 | 32))) {
@@ -288,8 +317,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[g & 1], bfr[s & 1][j], acc[i][j], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
-          if (late && issue && g == NG / 2 - 1 && !(EOSV_ABL(a) & 1)) {
-            stage((kt + NS - 1) * BK, wslot, EOSV_ABL(a));
+          if (late && g == NG / 2 - 1) {
+            issue_step(kt);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -325,7 +354,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
         }
     }
     // stage kt + 1 must have landed; the ones issued after it (up to kt + NS - 1) may fly on
-    wait_stages(min(NS - 2, nk - 2 - kt));
+    // (split rings: A(kt + 2), when issued)
+    if constexpr (NSA > 0) {
+      if (kt + 2 < nk)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(AI) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      wait_stages(min(NS - 2, nk - 2 - kt));
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -353,7 +390,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // 5-25 % of a layer).
   constexpr int EPR = WM * 32;   // rows per pass
   constexpr int EPS = BN + 4;    // f32 row stride
-  static_assert(EPR * EPS * 4 <= NS * STAGE * 2, "epilogue tile must fit the ring");
+  static_assert(EPR * EPS * 4 <= SMEM * 2, "epilogue tile must fit the ring");
   float* ep = (float*)smem;
   float bcol[TN];
 #pragma unroll
@@ -467,37 +504,47 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 #ifndef EOSV_BF16_K32
 #define EOSV_BF16_K32 0
 #endif
+// 256x256 tiles with split rings (3 A slots, 2 B slots: A two K-steps ahead), all of the LDS:
+// 1 (default) for the convs that gain (below), 2 for every 256x256 conv, 0 never
+#ifndef EOSV_BF16_ARING
+#define EOSV_BF16_ARING 1
+#endif
+// Cout 128 stride-2 convs on 256x128 tiles with split rings (the 512x128 tile's A slots do not
+// fit three times): r03 A/B 10-17 % slower than 512x128 (R50 layer2.0 conv2, R18 layer2.0 conv1)
+#ifndef EOSV_BF16_C128_ARING
+#define EOSV_BF16_C128_ARING 0
+#endif
 
 static int bf16_rows() {
   static int v = env_switch("EOSV_BF16_ROWS", 1);  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, bool STEM, int NS = 2, int BK = 64>
+template <int BM, int BN, int WM, int WN, bool STEM, int NS = 2, int BK = 64, int NSA = 0>
 static int launch_bf16(const ConvArgs& a, hipStream_t s) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
   if (a.plan) {
     static const int occ =
-        kernel_occupancy((const void*)conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, false, BK>, 64 * WM * WN);
+        kernel_occupancy((const void*)conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, false, BK, NSA>, 64 * WM * WN);
     return record_launch(a.plan, nb, occ);
   }
   if (a.split) {
     if (STEM || (a.x2 && (a.K1 % 64 || a.Cin2 % 64)))
       return set_error("conv_bf16: split layout shape"), EOSV_ERR_UNSUPPORTED;
     if (a.x2)
-      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, true, BK>), dim3((unsigned)nb),
+      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, true, BK, NSA>), dim3((unsigned)nb),
                          dim3(64 * WM * WN), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, true, BK>), dim3((unsigned)nb),
+      hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, false, true, BK, NSA>), dim3((unsigned)nb),
                          dim3(64 * WM * WN), 0, s, a);
   } else if (a.x2) {
     if (STEM || a.K1 % 64 || a.Cin2 % 64) return set_error("conv_bf16: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, false, BK>), dim3((unsigned)nb),
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, false, 16, NS, true, false, BK, NSA>), dim3((unsigned)nb),
                        dim3(64 * WM * WN), 0, s, a);
   } else {
-    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS, false, false, BK>), dim3((unsigned)nb),
+    hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, WM, WN, STEM, 16, NS, false, false, BK, NSA>), dim3((unsigned)nb),
                        dim3(64 * WM * WN), 0, s, a);
   }
   EOSV_LAUNCH_CHECK();
@@ -546,11 +593,20 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
 #endif
   if (a.Cout == 128) {
     if constexpr ((EOSV_BF16_K32 & 4) != 0) return launch_bf16<512, 128, 4, 2, false, 4, 32>(a, s);
+    if constexpr (EOSV_BF16_C128_ARING != 0)
+      if (a.stride != 1) return launch_bf16<256, 128, 4, 2, false, 2, 64, 3>(a, s);
     return launch_bf16<512, 128, 4, 2, false>(a, s);
   }
   if (a.Cout >= 256) {
     if constexpr ((EOSV_BF16_K32 & 1) != 0) return launch_bf16<256, 256, 2, 4, false, 4, 32>(a, s);
     if constexpr ((EOSV_BF16_K32 & 2) != 0) return launch_bf16<256, 256, 2, 4, false, 5, 32>(a, s);
+    // split rings (A two K-steps ahead) for the 1x1s, the stride-2 3x3s and the fused-downsample
+    // convs; the stride-1 3x3s keep the one ring (r03 A/B, ms per 3200 frames, R50: 1x1s 6-11 %
+    // faster, e.g. stage-4 conv1 0.33 -> 0.29, 1x1 + downsample 1.15 -> 1.08, stride-2 3x3 0.67 ->
+    // 0.64; stride-1 3x3s 2-4 % slower with them)
+    if constexpr (EOSV_BF16_ARING != 0)
+      if (EOSV_BF16_ARING == 2 || a.KH * a.KW == 1 || a.stride != 1 || a.x2)
+        return launch_bf16<256, 256, 2, 4, false, 2, 64, 3>(a, s);
     return launch_bf16<256, 256, 2, 4, false>(a, s);
   }
   return launch_bf16<128, 64, 2, 2, false>(a, s);
