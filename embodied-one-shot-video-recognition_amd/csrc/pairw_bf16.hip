@@ -12,9 +12,10 @@
 // The stage-1 pair (pair1x1_bf16.hip) keeps both weight matrices in LDS; here they are 128 KB
 // to 512 KB each, so they stream through LDS instead and Y never leaves registers:
 //   * persistent workgroups of 8 waves (one per CU); a round is 128 pixels, 16 per wave;
-//   * the CEXP channels go in chunks of 64: a 2-slot LDS ring holds a chunk's W3 rows
-//     (64 x CMID) and W1 columns (C1 x 64), filled by LDS-DMA one chunk ahead, one barrier per
-//     chunk; every wave reads the same slot for its own 16 pixels;
+//   * the CEXP channels go in chunks of 64: an LDS ring holds a chunk's W3 rows (64 x CMID) and
+//     W1 columns (C1 x 64), filled by LDS-DMA two chunks ahead in 3 slots where they fit (stage
+//     2: 100 / 146 KiB), else one chunk ahead in 2, one barrier per chunk; every wave reads the
+//     same slot for its own 16 pixels;
 //   * GEMM1 per chunk: D1[64 cout][16 px] = W3c . X^T on v_mfma_f32_16x16x32_bf16, the X
 //     fragments of the wave's pixels held in registers for the whole round; W3 rows are permuted
 //     (MFMA tile i, row 4q + e holds cout 32(i >> 1) + 8q + 4(i & 1) + e, as in pair1x1_bf16) so
@@ -81,7 +82,9 @@ struct PairW {
   static constexpr int XS = K3 / 32;    // X fragments (k-slices of GEMM1) per lane
   static constexpr int XSM = CMID / 32;  // ... of them from x (the rest from x2)
   static constexpr int G2 = C1 / 64;    // 64-cout groups of GEMM2
-  static constexpr int LDS = 2 * STAGE + C1 * 4;
+  // weight ring: 3 slots (DMA two chunks ahead) where they fit beside the conv1 shifts, else 2
+  static constexpr int NSLOT = 3 * STAGE + C1 * 4 <= 163840 ? 3 : 2;
+  static constexpr int LDS = NSLOT * STAGE + C1 * 4;
   static_assert(STAGE_W % (1024 * NW) == 0 && W3B % 1024 == 0 && PPW >= 2, "DMA pieces");
   static_assert(NCH % 4 == 0, "ring slots / residual ring");
   static_assert(PPW < XS + 2 * G2, "DMA pieces go out one per fragment group, the residual loads after them");
@@ -96,7 +99,8 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   constexpr int K3 = P::K3, XSM = P::XSM;
   constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW, NT = 64 * P::NW;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS];
-  float* const b1s = (float*)(smem + 2 * P::STAGE);
+  constexpr int NSLOT = P::NSLOT;
+  float* const b1s = (float*)(smem + NSLOT * P::STAGE);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -199,8 +203,13 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   constexpr int NRES = DSC ? 0 : 2 * NPT;  // residual loads per chunk
   RoundRes cur = round_res(rt);
   v4u xf[NPT][XS], rres[4][NPT][2];
+  int rslot = 0;  // NSLOT 3: ring slot of the current chunk (chunk count mod 3)
 #pragma unroll
   for (int j = 0; j < PPW; ++j) dma_piece(j, 0, 0);
+  if constexpr (NSLOT == 3) {  // chunk 1 too (the ring runs two chunks ahead)
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) dma_piece(j, 1 % NCH, 1);
+  }
   load_x(cur, rt, xf);
   if constexpr (!DSC) {
 #pragma unroll
@@ -217,13 +226,16 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc2[t][g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // chunk quads: the ring slot and the residual register set are compile-time per step
+    // chunk quads: the residual register set (and with 2 slots the ring slot) are compile-time
+    // per step; with 3 slots the slot of chunk ch is the workgroup's chunk count mod 3 (rslot),
+    // and chunk ch + 2 goes into rslot + 2 mod 3 (the slot chunk ch - 1 was read from)
 #pragma unroll 1
     for (int cp = 0; cp < NCH; cp += 4)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int ch = cp + u;
-      const int slot = u & 1;
+      const int slot = NSLOT == 3 ? rslot : u & 1;
+      const int wslot = NSLOT == 3 ? (rslot == 0 ? 2 : rslot - 1) : slot ^ 1;
       // This wave's DMA of chunk ch is done, then every wave's (barrier): the slot is complete,
       // and slot ^ 1 (chunk ch - 1) is free for the next chunk's DMA.  In chunk ch - 1 the DMA
       // pieces went out with its first PPW fragment groups (one per group: an LDS-DMA issue costs
@@ -239,17 +251,24 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       // store still in flight here only makes the wait stricter (measured: stage-2 pairs 1.43 ->
       // 1.55 ms, stage-3 0.81 -> 0.87 per 3200 frames; deferring the Y stores by a chunk, to have
       // them retired by then, gave wrong results and was dropped).
+      // 3 slots: chunk ch's pieces went out two chunks ago; younger than them are at least that
+      // chunk's residual loads and the last chunk's pieces and residual loads (the first two
+      // chunks of the launch have more: the prologue's X and residual loads), so the wait no
+      // longer depends on the stores issued since
       constexpr int YOUNG = NRES;
       constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0);
       constexpr int YOUNG_PRO = XS * NPT + (DSC ? 0 : 2 * RD * NPT);
-      if (u == 0)
+      if constexpr (NSLOT == 3)
+        vm_wait<PPW + 2 * NRES>();
+      else if (u == 0)
         vm_wait<(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST)>();
       else
         vm_wait<YOUNG>();
       if (!(abl & 16)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of the slot moves above the barrier (s_barrier is not a compiler memory barrier)
       __builtin_amdgcn_sched_barrier(0);
-      const int nch = ch + 1 < NCH ? ch + 1 : 0;  // the last chunk prefetches the next round's chunk 0
+      // the chunk whose weights this one prefetches (the round's last one(s): the next round's first)
+      const int nch = NSLOT == 3 ? (ch + 2 < NCH ? ch + 2 : ch + 2 - NCH) : (ch + 1 < NCH ? ch + 1 : 0);
 
       const unsigned char* ws = smem + slot * P::STAGE;
       // The chunk's A fragments come in NG groups of 4 (GEMM1 slices s = 0 .. XS - 1: W3 tiles
@@ -281,7 +300,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       bf16x8 yf[NPT][2];
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
-        if (gi < PPW && !(abl & 1)) dma_piece(gi, nch, slot ^ 1);
+        if (gi < PPW && !(abl & 1)) dma_piece(gi, nch, wslot);
         if (!DSC && gi == PPW && !(abl & 2)) {  // branch-free (scalar selects): a branch here made hipcc wait vmcnt(0) at the join
           const bool here = ch + RD < NCH;
           RoundRes rr;
@@ -348,6 +367,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      if constexpr (NSLOT == 3) rslot = rslot == 2 ? 0 : rslot + 1;
     }
     // epilogue 2: + shift, ReLU, bf16 -> Z
 #pragma unroll
