@@ -228,6 +228,28 @@ def test_backbone_batch_invariance(dtype, name):
     assert torch.equal(a[21:22], d)
 
 
+@pytest.mark.parametrize("dtype,name", [("bf16", "resnet50"), ("f32x3", "resnet50"), ("bf16", "resnet18")])
+def test_backbone_repeat_determinism(dtype, name):
+    """The same batch through the same handle, again and again: every stage's map bitwise equal
+    run to run (tools/race_probe.py in a test).  37 frames leave a tail in every persistent
+    kernel's last round; r03's wide-pair tail round changed the last frame's stage-3/4 features
+    in 16 of 16 runs before its fix (Determinism)."""
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    x = torch.randn(37, 3, 224, 224, generator=torch.Generator().manual_seed(5)).cuda()
+    bb = engine.Backbone(name, dtype, 224, 224, max_frames=37)
+    bb.load_state_dict(sd)
+    try:
+        for stage in (2, 3, 4):
+            ref = bb.probe(x, stage)
+            for _ in range(6):
+                assert torch.equal(bb.probe(x, stage), ref), f"stage {stage} changed between identical runs"
+        ref = bb.forward(x)
+        for _ in range(6):
+            assert torch.equal(bb.forward(x), ref)
+    finally:
+        bb.close()
+
+
 def test_full_size_c2_f32_bf16_agreement():
     """Config 2 at its full shape (224², T=16, R18, 400 episodes = 38,400 frames through
     the chunked forward): f32 and bf16 predict the same class on >= 97 % of the episodes,
