@@ -59,11 +59,6 @@ __device__ __forceinline__ void dma16(const unsigned char* src, void* lds) {
 }  // namespace
 
 constexpr int PW_TILE = PAIRW_TILE;  // pixels per round
-// 2-slot residual pairs (stage 3): each chunk's Y stores go out at the next chunk's start, from
-// inline asm (DEFER in the kernel); 0 = stored in the epilogue
-#ifndef EOSV_PAIRW_DEFER
-#define EOSV_PAIRW_DEFER 1
-#endif
 
 // NPT: 16-pixel tiles per wave.  NPT = 1: 8 waves (two per SIMD); NPT = 2: 4 waves (one per SIMD,
 // 512 VGPRs) that read each LDS weight fragment once for 32 pixels -- the LDS feeds one fragment per
@@ -209,34 +204,6 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   RoundRes cur = round_res(rt);
   v4u xf[NPT][XS], rres[4][NPT][2];
   int rslot = 0;  // NSLOT 3: ring slot of the current chunk (chunk count mod 3)
-  // DEFER (2 slots, residual pairs): a chunk's Y stores go out right after the next chunk's
-  // barrier, a chunk ahead of the wait they could hold up (the wait counts loads only, so a store
-  // still in flight there drains the residual prefetch).  They are inline asm: hipcc's own waits
-  // for a loaded value count every VMEM op issued after the load as retiring in order with it,
-  // and with the stores as builtins issued at the chunk's start its wait for the residual let
-  // the first chunk after the loop back edge use a residual not yet landed (wrong results
-  // whenever a workgroup ran several rounds); invisible to hipcc, the asm stores only make its
-  // waits stricter.  The s_nop covers the 16-B store's data-VGPR hazard (hipcc inserts it only for
-  // its own stores) and the empty asm in the epilogue keeps the data until the next overwrite.
-  // r03, per 3200 frames: stage-3 pairs 0.87 -> 0.78-0.81 ms; the downsample pair (no residual
-  // loads to drain) was 6 % slower with it and keeps its stores in the epilogue.
-  constexpr bool DEFER = NSLOT == 2 && DSC == 0 && EOSV_PAIRW_DEFER;
-  v4u ypend[NPT][2];
-  int yvoff[NPT];
-#pragma unroll
-  for (int t = 0; t < NPT; ++t) {
-    ypend[t][0] = ypend[t][1] = v4u{0, 0, 0, 0};
-    yvoff[t] = 0;
-  }
-  __amdgpu_buffer_rsrc_t yrs = rsrc(a.y, 0);  // first chunk: nothing pending (empty record)
-  auto store_ypend = [&]() {
-#pragma unroll
-    for (int t = 0; t < NPT; ++t)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"
-                     ::"v"(ypend[t][hh]), "v"(yvoff[t]), "s"(yrs), "i"(64 * hh) : "memory");
-  };
 #pragma unroll
   for (int j = 0; j < PPW; ++j) dma_piece(j, 0, 0);
   if constexpr (NSLOT == 3) {  // chunk 1 too (the ring runs two chunks ahead)
@@ -300,10 +267,6 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       if (!(abl & 16)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of the slot moves above the barrier (s_barrier is not a compiler memory barrier)
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DEFER) {
-        if (!(abl & 4)) store_ypend();
-        __builtin_amdgcn_sched_barrier(0);
-      }
       // the chunk whose weights this one prefetches (the round's last one(s): the next round's first)
       const int nch = NSLOT == 3 ? (ch + 2 < NCH ? ch + 2 : ch + 2 - NCH) : (ch + 1 < NCH ? ch + 1 : 0);
 
@@ -396,20 +359,10 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
                 }
                 pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
               }
-              if constexpr (DEFER) {
-                asm volatile("" ::"v"(ypend[t][hh]));  // the deferred store's data stays put until here
-                ypend[t][hh] = pk;
-              } else if (!(abl & 4)) {
+              if (!(abl & 4))
                 __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2, (ch * 64 + 32 * hh) * 2, 0);
-              }
               yf[t][hh] = __builtin_bit_cast(bf16x8, pk);
             }
-          }
-          if constexpr (DEFER) {
-            asm volatile("" ::"v"(yvoff[0]), "s"(yrs));
-            yrs = cur.y;
-#pragma unroll
-            for (int t = 0; t < NPT; ++t) yvoff[t] = ((pw + 16 * t) * CEXP + 8 * q + ch * 64) * 2;
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -436,8 +389,6 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
         }
     cur = nxt;
   }
-  if constexpr (DEFER)
-    if (!(abl & 4)) store_ypend();  // the last chunk's Y
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) chunk-0 prefetch has landed
 }
 
