@@ -228,7 +228,8 @@ def test_backbone_batch_invariance(dtype, name):
     assert torch.equal(a[21:22], d)
 
 
-@pytest.mark.parametrize("dtype,name", [("bf16", "resnet50"), ("f32x3", "resnet50"), ("bf16", "resnet18")])
+@pytest.mark.parametrize("dtype,name", [("bf16", "resnet50"), ("f32x3", "resnet50"), ("bf16", "resnet18"),
+                                        ("bf16", "resnet101")])
 def test_backbone_repeat_determinism(dtype, name):
     """The same batch through the same handle, again and again: every stage's map bitwise equal
     run to run (tools/race_probe.py in a test).  37 frames leave a tail in every persistent
