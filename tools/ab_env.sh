@@ -18,5 +18,5 @@ for round in $(seq ${ROUNDS:-2}); do
   done
 done
 set -- $VALS
-paste $(for v in $VALS; do echo gpurun_out/ab_${VAR}_$v.log; done) 2>/dev/null | grep "^layer" | \
-  awk -F'\t' '{printf "%s", substr($1, 1, 10); for (i = 1; i <= NF; ++i) { split($i, f, " "); printf "  %8s ms %8s TF", f[3], f[5] } printf "\n"}'
+paste $(for v in $VALS; do echo gpurun_out/ab_${VAR}_$v.log; done) 2>/dev/null | grep "] layer" | \
+  awk -F'\t' '{split($1, h, " "); printf "layer %3s", h[3]; for (i = 1; i <= NF; ++i) { split($i, f, " "); printf "  %8s ms %8s TF", f[4], f[6] } printf "\n"}'
