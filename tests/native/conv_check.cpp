@@ -658,6 +658,12 @@ int main() {
   fails += check_bf16(5, 14, 14, 1024, 256, 1, 1, 0, false, true);
   fails += check_bf16(5, 14, 14, 256, 1024, 1, 1, 0, true, true);
   fails += check_bf16(2, 9, 11, 128, 128, 3, 1, 1, true, false);  // ragged map, M = 198
+  // halo-staged stride-1 3x3s (conv_halo_bf16, kcm weights, Cout % 256 == 0): 16x16 / 8x8 maps
+  // (256x256 input), a ragged map with an M tail, Cout 512 (two cout tiles)
+  fails += check_bf16(7, 16, 16, 256, 256, 3, 1, 1, true, true, true);
+  fails += check_bf16(5, 8, 8, 512, 512, 3, 1, 1, false, true, true);
+  fails += check_bf16(3, 10, 12, 128, 256, 3, 1, 1, true, false, true);
+  fails += check_bf16(11, 7, 7, 256, 512, 3, 1, 1, true, true, true);
   fails += check(1, 8, 8, 32, 64, 1, 1, 0, false, false, false);
   fails += check(2, 9, 7, 64, 64, 3, 1, 1, false, false, false);
   fails += check(2, 14, 14, 64, 128, 3, 2, 1, false, true, true);
