@@ -137,8 +137,6 @@ int launch_conv_f32(const ConvArgs& a, hipStream_t s);
 int launch_conv_bf16(const ConvArgs& a, hipStream_t s);
 bool conv_bf16_ts_ok(const ConvArgs& a);  // conv_bf16_ts.hip: tap-shift stride-1 3x3 convs
 int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s);
-bool conv_halo_bf16_ok(const ConvArgs& a);  // conv_halo_bf16.hip: halo-staged stride-1 3x3s, Cout % 256 == 0
-int launch_conv_halo_bf16(const ConvArgs& a, hipStream_t s);
 bool stem_pool_bf16_ok(int H, int W, bool direct);  // stem_pool_bf16.hip: fused stem conv + ReLU + maxpool
 int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, const float* bias, void* y,
                           hipStream_t s, const float* frames = nullptr, LaunchInfo* info = nullptr);

@@ -515,12 +515,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 #define EOSV_BF16_C128_ARING 0
 #endif
 
-// stride-1 3x3 convs with Cout % 256 == 0 on maps of <= 512 halo slots per 256-pixel tile on
-// conv_halo_bf16.hip (1) or on the 256x256 implicit GEMM (0)
-#ifndef EOSV_BF16_HALO
-#define EOSV_BF16_HALO 0
-#endif
-
 static int bf16_rows() {
   static int v = env_switch("EOSV_BF16_ROWS", 1);  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
   return v;
@@ -597,9 +591,6 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return launch_bf16<256, 128, 2, 2, false>(a, s);
   }
 #endif
-  // halo-staged kernel for the stride-1 3x3s with Cout % 256 == 0 on small maps (stages 3-4)
-  static const int halo = env_switch("EOSV_BF16_HALO", EOSV_BF16_HALO);
-  if (halo && conv_halo_bf16_ok(a)) return launch_conv_halo_bf16(a, s);
   if (a.Cout == 128) {
     if constexpr ((EOSV_BF16_K32 & 4) != 0) return launch_bf16<512, 128, 4, 2, false, 4, 32>(a, s);
     if constexpr (EOSV_BF16_C128_ARING != 0)
