@@ -127,8 +127,8 @@ def cpu_baseline(args, batch, T, emb, preds):
 
 
 def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
-    """Warmup + timed region for one backbone dtype; returns (elapsed_s, preds, per-layer profile,
-    clip embeddings of the last step)."""
+    """Warmup + timed region for one backbone dtype; returns (max-over-ranks elapsed_s, every rank's
+    elapsed_s, preds, per-layer profile, clip embeddings of the last step)."""
     bb = engine.Backbone(args.arch, dtype, args.res, args.res, max_frames=args.max_frames, device=local)
     bb.load_state_dict(synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
     feat = torch.empty(max(d.batch.n_frames for d in batches), bb.D, device=f"cuda:{local}")
@@ -155,8 +155,8 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     bb.profile(False)
     bb.close()
     from eosv import dist as edist
-    run_timed.per_rank_elapsed = edist.gather_values(elapsed)
-    return max(run_timed.per_rank_elapsed), torch.cat(preds), prof, emb.cpu().numpy()
+    per_rank = edist.gather_values(elapsed)
+    return max(per_rank), per_rank, torch.cat(preds), prof, emb.cpu().numpy()
 
 
 def measured_traffic(dtype, key):
@@ -298,12 +298,22 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} ranks", file=sys.stderr)
     # one rank per GPU; more ranks than devices share them round-robin (gloo rehearsals only)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-    dist = world > 1
+    # a process group for N > 1, or at N = 1 when a backend is named (EOSV_DIST_BACKEND=nccl runs
+    # the RCCL path -- barrier, all-gathers, all-reduce -- on one GPU; MASTER_ADDR / MASTER_PORT
+    # must then be set, as under a launcher)
+    dist = world > 1 or bool(os.environ.get("EOSV_DIST_BACKEND"))
     torch.cuda.set_device(local)
     if dist:
         import torch.distributed as tdist
-        backend = os.environ.get("EOSV_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
-        tdist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
+        backend = os.environ.get("EOSV_DIST_BACKEND") or "nccl"  # nccl == RCCL on ROCm
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:  # N = 1 without a launcher: a free local port
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        tdist.init_process_group(backend, rank=rank, world_size=world,
+                                 device_id=torch.device("cuda", local) if backend == "nccl" else None)
     from eosv import arch as arch_mod, dist as edist, engine, episodes as ep_mod, synth  # noqa
 
     T = args.segments * args.seg_len
@@ -319,8 +329,7 @@ def main():
     torch.cuda.synchronize()
     timed_idx = mine_idx[args.warmup * E:]
 
-    elapsed, pred, prof, emb = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
-    per_rank_elapsed = run_timed.per_rank_elapsed
+    elapsed, per_rank_elapsed, pred, prof, emb = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
     per_rank_clips = [int(v) for v in edist.gather_values(sum(d.batch.n_clips for d in batches[args.warmup:]))]
     clips = sum(per_rank_clips)
     frames_rank = sum(d.batch.n_frames for d in batches[args.warmup:])
@@ -333,7 +342,7 @@ def main():
 
     legs = []
     for dt2 in [d for d in (args.secondary_dtype or "").split(",") if d and d not in ("none", args.dtype)]:
-        el2, pred2, prof2, emb2 = run_timed(args, engine, arch_mod, synth, batches, dt2, local, dist)
+        el2, _, pred2, prof2, emb2 = run_timed(args, engine, arch_mod, synth, batches, dt2, local, dist)
         # clip embeddings of the last step vs the f32 primary: max over clips of
         # max|e - e_f32| / max|e_f32| (the north star's 1e-4 relative bound, tests/test_gpu_parity.py)
         if args.layers and rank == 0:

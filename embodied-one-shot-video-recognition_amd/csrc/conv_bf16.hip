@@ -252,10 +252,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   // issues its DMA in the middle of the K-step (after half of its MFMA groups) instead of at its
   // start, so that each SIMD pairs one wave's DMA issue with the other's MFMAs (r03, R50 bf16 per
   // 3200 frames: 3x3 convs 4-7 % faster, 1x1s unchanged, the 1x1 + folded-downsample convs 6-8 %
-  // slower, so those keep the plain order unless bit 2); bit 1: s_setprio 1 for the upper half
-  // (measured slower).
+  // slower, so those keep the plain order unless bit 2); bit 1 (profiling build only): s_setprio 1
+  // for the upper half (measured slower).
   const bool late = (EOSV_BF16_STAG & 1) && MF == 16 && (!DS || a.KH > 1 || (EOSV_BF16_STAG & 4)) && wid >= NW / 2;
+#ifdef EOSV_PROFILING
   if ((EOSV_BF16_STAG & 2) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // the K-step's DMA: one ring: stage kt + NS - 1 into slot wslot; split rings: B(kt + 1) then
   // A(kt + 2) (in this order: the end-of-step wait leaves only A(kt + 2) in flight)
   auto issue_step = [&](int kt) {
@@ -496,23 +498,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
   }
 }
 
-// Ring shape of the 256x256 / 512x128 im2col tiles: 0 = 64-deep K-steps in a 2-slot ring;
-// bit 0 (256x256) / bit 2 (512x128): 32-deep K-steps in a 4-slot ring; bit 1: 256x256 in 5 slots.
-// r03 A/B (R50 bf16, ms per 3200 frames): the 32-deep rings are 12-20 % slower on every 3x3 conv
-// (0.63 -> 0.74-0.80), whatever the depth: two or three K-steps in flight do not pay for the
-// 64-B rows (twice the row segments per staged byte); kept as a build option only.
-#ifndef EOSV_BF16_K32
-#define EOSV_BF16_K32 0
-#endif
 // 256x256 tiles with split rings (3 A slots, 2 B slots: A two K-steps ahead), all of the LDS:
-// 1 (default) for the convs that gain (below), 2 for every 256x256 conv, 0 never
+// 1 (default) for the convs that gain (below), 2 for every 256x256 conv, 0 never.  (Rejected in r03
+// and removed from the source: 32-deep K-steps in 4/5-slot rings, 12-20 % slower on every 3x3; the
+// Cout-128 stride-2 convs on 256x128 split-ring tiles, 10-17 % slower)
 #ifndef EOSV_BF16_ARING
 #define EOSV_BF16_ARING 1
-#endif
-// Cout 128 stride-2 convs on 256x128 tiles with split rings (the 512x128 tile's A slots do not
-// fit three times): r03 A/B 10-17 % slower than 512x128 (R50 layer2.0 conv2, R18 layer2.0 conv1)
-#ifndef EOSV_BF16_C128_ARING
-#define EOSV_BF16_C128_ARING 0
 #endif
 
 static int bf16_rows() {
@@ -591,15 +582,8 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return launch_bf16<256, 128, 2, 2, false>(a, s);
   }
 #endif
-  if (a.Cout == 128) {
-    if constexpr ((EOSV_BF16_K32 & 4) != 0) return launch_bf16<512, 128, 4, 2, false, 4, 32>(a, s);
-    if constexpr (EOSV_BF16_C128_ARING != 0)
-      if (a.stride != 1) return launch_bf16<256, 128, 4, 2, false, 2, 64, 3>(a, s);
-    return launch_bf16<512, 128, 4, 2, false>(a, s);
-  }
+  if (a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
   if (a.Cout >= 256) {
-    if constexpr ((EOSV_BF16_K32 & 1) != 0) return launch_bf16<256, 256, 2, 4, false, 4, 32>(a, s);
-    if constexpr ((EOSV_BF16_K32 & 2) != 0) return launch_bf16<256, 256, 2, 4, false, 5, 32>(a, s);
     // split rings (A two K-steps ahead) for the 1x1s, the stride-2 3x3s and the fused-downsample
     // convs; the stride-1 3x3s keep the one ring (r03 A/B, ms per 3200 frames, R50: 1x1s 6-11 %
     // faster, e.g. stage-4 conv1 0.33 -> 0.29, 1x1 + downsample 1.15 -> 1.08, stride-2 3x3 0.67 ->

@@ -36,9 +36,9 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
 }
 }  // namespace
 
-#ifndef EOSV_TS_STAG
-#define EOSV_TS_STAG 1
-#endif
+// DMA stagger of the upper half of the waves: they issue the stage's DMA after tap kw = TS_STAG - 1
+// (r03: 1, i.e. after the first tap; 0 = no stagger)
+constexpr int TS_STAG = 1;
 
 template <int BM, int BN, int WM, int WN, bool SPLIT>
 __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) {
@@ -174,11 +174,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   }
 
   const int nst = nst3 + (x2 ? a.Cin2 / BK : 0);
-  // EOSV_TS_STAG k > 0: the upper half of the waves (the partners w + NW/2 of a SIMD's pairs)
+  // TS_STAG k > 0: the upper half of the waves (the partners w + NW/2 of a SIMD's pairs)
   // issues its next-stage DMA after tap kw = k - 1 instead of at the stage's start (as
   // conv_bf16_kernel's stagger: one wave's DMA issue beside the other's MFMAs).  r03, R50 bf16
   // stage-2 3x3s per 3200 frames: k = 1 0.81-0.86 -> 0.77-0.82 ms (4-5 %), k = 2 1-2 %.
-  const int lkw = (EOSV_TS_STAG > 0 && wid >= NW / 2) ? EOSV_TS_STAG - 1 : -1;
+  const int lkw = (TS_STAG > 0 && wid >= NW / 2) ? TS_STAG - 1 : -1;
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();

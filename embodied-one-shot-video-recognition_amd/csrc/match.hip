@@ -241,8 +241,11 @@ __global__ __launch_bounds__(256) void seg_match_kernel(const float* __restrict_
     const float v = fmaf(l1, dp, fmaf(l2, dl[lr][gl], l1 * dm));
     if (out && g < G) out[(long long)row * G + g] = v;
     // order-preserving key of the float (negative values, e.g. from lamda1/lamda2 < 0 set in
-    // utils, flip all bits; the others get the sign bit), -0 folded into +0 as argsort ties them
-    const unsigned vb = __float_as_uint(v == 0.f ? 0.f : v);
+    // utils, flip all bits; the others get the sign bit), -0 folded into +0 as argsort ties them,
+    // and every NaN canonicalised to +qNaN first, so that it keys above +inf whatever its sign
+    // (np.argsort puts NaNs last; a negative NaN would otherwise flip below -inf)
+    const float vc = v != v ? __uint_as_float(0x7fc00000u) : v;
+    const unsigned vb = __float_as_uint(vc == 0.f ? 0.f : vc);
     const unsigned ob = (vb & 0x80000000u) ? ~vb : (vb | 0x80000000u);
     unsigned long long key = g < G ? ((unsigned long long)ob << 32) | (unsigned)g : ~0ull;
 #pragma unroll

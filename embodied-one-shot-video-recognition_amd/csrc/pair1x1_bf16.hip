@@ -39,6 +39,11 @@ typedef unsigned short u16;
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)v << 16); }
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ (row & 7)) * 8; }
+// a tile's buffer resource: num_records 0 past the last tile, so the final prefetch reads zeros
+// without touching memory (as pairw_bf16's rounds)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+}
 }  // namespace
 
 constexpr int PAIR_BM = 64;  // pixels per tile
@@ -94,16 +99,21 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
       *(v4u*)(W1s + row * 256 + swz(row, c)) = *(const v4u*)(w1 + (long long)row * 256 + c * 8);
     }
   }
-  // X (and the downsample's input) of tile t: thread chunk k -> pixel (tid + 256k) / 8 mod 64
+  // X (and the downsample's input) of tile t: thread chunk k -> pixel (tid + 256k) / 8 mod 64.
+  // Loads go through per-tile buffer resources with empty records past the last tile: the
+  // branch-free prefetch of the loop's last iteration then reads nothing.  (It used to re-read
+  // tile ntiles - 1, whose residual lines another workgroup is rewriting in place, y = res.)
   v4u xr[XL];
   auto load_x = [&](long long tt) {
     const long long p0 = tt * BM;
+    const int nb = tt < ntiles ? BM * 64 * 2 : 0;
+    const __amdgpu_buffer_rsrc_t rx = tile_rsrc(x + p0 * 64, nb);
+    const __amdgpu_buffer_rsrc_t rx2 = tile_rsrc((DS ? x2 : x) + p0 * 64, nb);
 #pragma unroll
     for (int k = 0; k < XL; ++k) {
       const int idx = tid + 256 * (k & 1);
       const int px = idx >> 3, c = idx & 7;
-      const u16* src = (DS && k >= 2) ? x2 : x;
-      xr[k] = *(const v4u*)(src + (p0 + px) * 64 + c * 8);
+      xr[k] = __builtin_amdgcn_raw_buffer_load_b128((DS && k >= 2) ? rx2 : rx, (px * 64 + c * 8) * 2, 0, 0);
     }
   };
   auto store_x = [&]() {
@@ -119,11 +129,13 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
   auto load_r = [&](long long tt) {
     if constexpr (!DS) {
       const long long p0 = tt * BM;
+      const __amdgpu_buffer_rsrc_t rres = tile_rsrc(res + p0 * 256, tt < ntiles ? BM * 256 * 2 : 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
-          rr[2 * j + hh] = *(const v4u*)(res + (p0 + 16 * j + r) * 256 + 64 * w + 32 * hh + 8 * q);
+          rr[2 * j + hh] = __builtin_amdgcn_raw_buffer_load_b128(rres, ((16 * j + r) * 256 + 8 * q) * 2,
+                                                                 (64 * w + 32 * hh) * 2, 0);
     }
   };
   load_x(t);
@@ -133,9 +145,9 @@ __global__ __launch_bounds__(256) void pair1x1_bf16_kernel(Pair1x1Args a) {
 
   for (; t < ntiles; t += gridDim.x) {
     const long long p0 = t * BM;
-    // the next tile (the last one again past the end: branch-free, so the compiler counts the
-    // loads in flight instead of draining them at the join)
-    const long long tn = t + gridDim.x < ntiles ? t + gridDim.x : ntiles - 1;
+    // the next tile (past the end: empty records, branch-free, so the compiler counts the loads
+    // in flight instead of draining them at the join)
+    const long long tn = t + gridDim.x;
     // (A): X tile (and, first time round, the weights) in LDS; the previous tile's GEMM2 is done with Ys
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

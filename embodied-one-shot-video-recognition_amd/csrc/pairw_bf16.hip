@@ -91,8 +91,12 @@ struct PairW {
 };
 
 // ABL (profiling-only instance, EOSV_CONV_ABL bits; results wrong): 1 no weight DMA, 2 no
-// residual loads, 4 no Y stores, 8 no MFMAs, 16 no chunk barriers, 32 no Z stores, 64 no X loads
-template <int CMID, int CEXP, int C1, int NPT, int DSC, bool ABL = false>
+// residual loads, 4 no Y stores, 8 no MFMAs, 16 no chunk barriers, 32 no Z stores, 64 no X loads.
+// CS: the chunk waits count the Y / Z stores issued after a slot's last DMA piece among the younger
+// ops (vmcnt retires loads, stores and LDS-DMA together in issue order, MI355X_MICROARCH.md), so
+// they do not drain the residual prefetch; without CS they count loads only (r03), which is
+// stricter whenever a store is still in flight.
+template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false>
 __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   using P = PairW<CMID, CEXP, C1, NPT, DSC>;
   const int abl = ABL ? a.abl : 0;
@@ -255,12 +259,26 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
       // chunk's residual loads and the last chunk's pieces and residual loads (the first two
       // chunks of the launch have more: the prologue's X and residual loads), so the wait no
       // longer depends on the stores issued since
-      constexpr int YOUNG = NRES;
-      constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0);
+      // 2 slots, the rule (r04): the count may include the round's X loads only where chunk ch - 1
+      // issued them, i.e. at the round's first chunk (cp == 0: ch - 1 was the previous round's
+      // last chunk, or the prologue ran).  Until r04 every u == 0 chunk used that count, also at
+      // cp = 4, 8, 12 where chunk ch - 1 (u == 3 of the previous quad) issued only its NRES residual
+      // loads after its pieces: stage 3 then waited vmcnt(10) with PPW = 8 pieces + 2 residual
+      // loads younger than the slot's oldest piece, i.e. for none of them, and the barrier let the
+      // waves read a slot still being filled (the stage-2 DSC pair: vmcnt(12) against 8 pieces).
+      // That hole explains every recorded failure (r03): the stage-2 pair of conv_check on 2 slots
+      // (NCH 8, the hole at cp = 4) one run in three, R50 / R101 stage 3 (NCH 16: cp = 4, 8, 12)
+      // in the race probes, and why vmcnt_probe -- which waited correctly -- found nothing.
+      // With CS the 2 NPT Y stores of a chunk count too when its epilogue (after group XS - 1)
+      // follows its last piece, and the round's 2 G2 NPT Z stores at a round's first chunk.
+      constexpr int YS = CS && XS >= PPW ? 2 * NPT : 0;
+      constexpr int YOUNG = NRES + YS;
+      constexpr int YOUNG_LAST = YOUNG + (XS >= PPW ? XS * NPT : 0) + (CS ? 2 * G2 * NPT : 0);
       constexpr int YOUNG_PRO = XS * NPT + (DSC ? 0 : 2 * RD * NPT);
-      if constexpr (NSLOT == 3)
-        vm_wait<PPW + 2 * NRES>();
-      else if (u == 0)
+      static_assert(YOUNG_LAST < 64 && PPW + 2 * NRES + 2 * YS < 64, "vmcnt range");
+      if constexpr (NSLOT == 3)  // younger: chunk ch - 2's residual loads (+ Y), chunk ch - 1's pieces, residual loads (+ Y)
+        vm_wait<PPW + 2 * NRES + 2 * YS>();
+      else if (u == 0 && cp == 0)  // scalar branch (cp is the unroll-1 loop's counter)
         vm_wait<(YOUNG_PRO < YOUNG_LAST ? YOUNG_PRO : YOUNG_LAST)>();
       else
         vm_wait<YOUNG>();
@@ -392,21 +410,29 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) chunk-0 prefetch has landed
 }
 
+#ifndef EOSV_PAIRW_CS
+#define EOSV_PAIRW_CS 1
+#endif
+
 template <int CMID, int CEXP, int C1, int NPT, int DSC = 0>
 static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
-  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC>, 512 / NPT);
+  constexpr bool CS = EOSV_PAIRW_CS;
+  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS>, 512 / NPT);
   const long long nrounds = (a.M + PW_TILE - 1) / PW_TILE;
   if (a.plan) return record_launch(a.plan, nrounds, occ);
   const long long grid = std::min<long long>(nrounds, (long long)occ * device_cu_count());
 #ifdef EOSV_PROFILING
   static const int abl = env_switch("EOSV_CONV_ABL", 0);
+  static const int cs = env_switch("EOSV_PAIRW_CS", CS);  // A/B of the wait rule
   if (abl) {
     Pair1x1Args b = a;
     b.abl = abl;
-    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, true>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, b);
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, true>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, b);
+  } else if (cs != CS) {
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, !CS>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
   } else
 #endif
-  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
+  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

@@ -15,20 +15,27 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("EOSV_LIBRARY") or os.path.join(PKG_ROOT, "libeosv.so")
 
 def source_digest() -> str:
-    """sha256 (16 hex) of the library's sources (csrc/*.hip, common.h, include/eosv.h): ties a
-    profile (e.g. profiles/*_traffic.json) to the kernels it measured; computable on the GPU box,
-    where there is no git history."""
+    """sha256 (16 hex) of the library's sources and build recipe (csrc/*.hip, common.h,
+    include/eosv.h, csrc/Makefile) plus the build-configuring environment (HIPCC flags and any
+    EOSV_* compile macro given through CXXFLAGS / EXTRA_FLAGS): ties a profile (e.g.
+    profiles/*_traffic.json) to the kernels it measured; computable on the GPU box, where there is
+    no git history."""
     import glob
     import hashlib
 
     h = hashlib.sha256()
     repo = os.path.dirname(PKG_ROOT)
     files = sorted(glob.glob(os.path.join(PKG_ROOT, "csrc", "*.hip"))) + \
-        [os.path.join(PKG_ROOT, "csrc", "common.h"), os.path.join(repo, "include", "eosv.h")]
+        [os.path.join(PKG_ROOT, "csrc", "common.h"), os.path.join(repo, "include", "eosv.h"),
+         os.path.join(PKG_ROOT, "csrc", "Makefile")]
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
+    for k in ("CXXFLAGS", "EXTRA_FLAGS", "HIPCC", "ARCH"):
+        v = os.environ.get(k)
+        if v:
+            h.update(f"{k}={v}".encode())
     return h.hexdigest()[:16]
 
 

@@ -641,7 +641,11 @@ def capture_wide(mods, only=None):
         "c5r101": lambda: capture_shaped(mods, "resnet50", "protonet", seed=41, episodes=5,
                                          tag="c5_r101_5w5s_t64_256_seed41_wide", n_way=5, k_shot=5, T=64, res=256,
                                          test_list="test_long64.list", backbone="resnet101", features=False),
-        "c3": lambda: capture_aug(mods, seed=9, episodes=30, tag="c3_r50_aug_seed9_wide", compact=True),
+        # round 4: 20 more R101 episodes (the round-3 five had no margin under 0.6)
+        "c5r101b": lambda: capture_shaped(mods, "resnet50", "protonet", seed=42, episodes=20,
+                                          tag="c5_r101_5w5s_t64_256_seed42_wide", n_way=5, k_shot=5, T=64, res=256,
+                                          test_list="test_long64.list", backbone="resnet101", features=False),
+        "c3":lambda: capture_aug(mods, seed=9, episodes=30, tag="c3_r50_aug_seed9_wide", compact=True),
     }
     make_long_list(os.path.join(REF, "sources/data/test.list"), os.path.join(OUT, "test_long64.list"), 64)
     for k, f in jobs.items():

@@ -31,7 +31,14 @@ SHAPED = ["c4_r50_14w1s_t32_seed7", "c5_r50_5w5s_t64_256_seed39", "c5_r101_5w5s_
 # (R50 / R101, sampled from tests/golden/test_long64.list: the reference cannot run a 256x256
 # episode that holds a video shorter than T, utils.py:252), compact form
 WIDE = ["c4_r50_14w1s_t32_seed8_wide", "c5_r50_5w5s_t64_256_seed40_wide", "c5_r101_5w5s_t64_256_seed41_wide"]
+# round 4: 20 more R101 episodes (capture_golden.py --wide c5r101b)
+WIDE += ["c5_r101_5w5s_t64_256_seed42_wide"]
 WIDE = [t for t in WIDE if os.path.exists(os.path.join(GOLDEN, t + ".json"))]
+# bf16 prediction agreement with the reference over many episodes (SURVEY section 7's rule, its
+# bound set to the evidence in r04: C2 measured 0.9985 over 2000 episodes, every wide fixture 1.000)
+BF16_MIN_AGREE = 0.97
+# C3 bf16 pool-id agreement (argmin over 5120 smoothed distances; measured 0.887-0.931)
+C3_BF16_MIN_POOL_AGREE = 0.85
 
 
 def _save_sd(name, path):
@@ -118,7 +125,7 @@ def test_wide_fixture(tag, dtype, tmp_path, monkeypatch):
     """Configs 4 / 5 over the wide reference fixtures (network_test.py:143-164 at 14w1s T32 and
     5w5s T64 256x256).  f32 and f32x3: every prediction bit-exact, embeddings within 1e-4 (through
     the projection bound), the result file's sha256 the reference's.  bf16 (config 5's stated
-    dtype; SURVEY section 7 rule): prediction agreement with the reference >= 0.9 and the accuracy
+    dtype; SURVEY section 7 rule, r04 bound): prediction agreement with the reference >= 0.97 and the accuracy
     within the 95 % binomial interval of the reference's, embeddings within 1e-2.  Prints the
     agreement, the near ties (top-2 margin < 1e-5) and the smallest margin."""
     meta, arr, got = _run_shaped(tag, tmp_path, monkeypatch, dtype)
@@ -135,7 +142,7 @@ def test_wide_fixture(tag, dtype, tmp_path, monkeypatch):
     assert worst <= 1.0
     if dtype == "bf16":
         half = 1.96 * math.sqrt(max(ref_acc * (1 - ref_acc), 1e-12) / E) + 1.0 / E
-        assert agree >= 0.9 and abs(acc - ref_acc) <= half
+        assert agree >= BF16_MIN_AGREE and abs(acc - ref_acc) <= half
     else:
         assert np.array_equal(got["preds"], ref_pred)
         assert hashlib.sha256(got["acc"].encode()).hexdigest() == meta["acc_file_sha256"]
@@ -204,7 +211,8 @@ def test_aug_segment_fast_legs(dtype, tmp_path, monkeypatch):
     backbone may pick another gallery segment where two are nearly equidistant.  Rule: wherever
     the pick differs from the reference's, the reference's own smoothed distance at the pick is
     within ``delta`` (relative) of its minimum -- bf16 1e-2 (its embedding error ~3e-3), f32x3 1e-4 --
-    and at least 80 % (bf16) / 95 % (f32x3) of the picks are identical.  Predictions identical."""
+    and at least 85 % (bf16, r04: measured 0.887-0.931) / 95 % (f32x3) of the picks are identical.
+    Predictions identical."""
     dbg, acc_text, meta, arr = _run_c3(tmp_path, monkeypatch, dtype)
     E = len(meta["episodes"])
     sm = arr["smoothed"]  # [E, 40, 5120] f32, the reference's temporal_convolution_flating_layer output
@@ -214,7 +222,7 @@ def test_aug_segment_fast_legs(dtype, tmp_path, monkeypatch):
     best = sm.min(axis=2)
     at_pick = np.take_along_axis(sm, got_pool[:, :, None], axis=2)[:, :, 0]
     slack = float(((at_pick - best) / np.abs(best)).max())
-    delta, min_agree = (1e-2, 0.8) if dtype == "bf16" else (1e-4, 0.95)
+    delta, min_agree = (1e-2, C3_BF16_MIN_POOL_AGREE) if dtype == "bf16" else (1e-4, 0.95)
     print(f"[c3 {dtype}] pool-id agreement {agree:.3f}, max relative slack at differing picks {slack:.2e}")
     assert slack <= delta, slack
     assert agree >= min_agree, agree
@@ -257,6 +265,10 @@ def test_aug_segment_eight_reference_episodes(tag, dtype, tmp_path, monkeypatch)
              if margins is not None else ""))
     if dtype == "f32":
         assert same.all()
+    elif dtype == "bf16":
+        assert same.mean() >= C3_BF16_MIN_POOL_AGREE, same.mean()
+    else:
+        assert same.mean() >= 0.95, same.mean()
     assert worst_slack <= delta
     sup = dbg["sup"].cpu().numpy().astype(np.float64).reshape(E, 45, -1)
     D = sup.shape[-1]
@@ -272,7 +284,7 @@ def test_aug_segment_eight_reference_episodes(tag, dtype, tmp_path, monkeypatch)
         acc, ref_acc = float((pred == qy).mean()), float((ref_pred == qy).mean())
         half = 1.96 * np.sqrt(max(ref_acc * (1 - ref_acc), 1e-12) / E) + 1.0 / E
         print(f"[c3 x{E} bf16] prediction agreement {(pred == ref_pred).mean():.3f}, acc {acc:.3f} vs {ref_acc:.3f}")
-        assert (pred == ref_pred).mean() >= 0.9 and abs(acc - ref_acc) <= half
+        assert (pred == ref_pred).mean() >= BF16_MIN_AGREE and abs(acc - ref_acc) <= half
     else:
         assert np.array_equal(pred, ref_pred)
         assert acc_text == meta["acc_file"]

@@ -177,3 +177,47 @@ def test_bench_spawns_ranks_and_matches_one_rank():
     assert sum(d2["per_rank_clips"]) == sum(d1["per_rank_clips"]) == 24 * 6
     clips = sum(d2["per_rank_clips"])
     assert abs(two["value"] - clips / max(d2["per_rank_elapsed_s"])) <= 0.01 * two["value"]
+
+
+# ------------------------------------------------------------------ RCCL (the "nccl" backend)
+_RCCL_ONE = r"""
+import os, sys
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+from eosv import dist as edist
+assert edist.describe() == {"backend": "nccl", "world_size_reported_by_backend": 1}, edist.describe()
+# the collectives bench.py and the drop-in drivers run, through RCCL on the device
+p = edist.gather_predictions([0, 2, 5], [4, 1, 3], 7)
+assert p.tolist() == [4, -1, 1, -1, -1, 3, -1], p
+x = torch.arange(48, dtype=torch.float32, device="cuda").reshape(6, 8)
+y = edist.all_gather_rows(x)
+assert y.device.type == "cuda" and torch.equal(y, x)
+assert edist.gather_values(2.5) == [2.5]
+assert edist.max_over_ranks(3.25) == 3.25 and edist.sum_over_ranks(11) == 11
+dist.barrier()
+dist.destroy_process_group()
+print("rccl ok")
+"""
+
+
+def test_rccl_world_size_one_collectives(tmp_path):
+    """The nccl (= RCCL) branch of eosv/dist.py executed on the device at world size 1: backend
+    reported, the (episode, prediction) all-gather, the row all-gather, the value all-gather and the
+    all-reduces (network_test.py:159-167 gathers its accuracies through these)."""
+    script = tmp_path / "rccl1.py"
+    script.write_text(_RCCL_ONE)
+    (out, err), = _spawn([sys.executable, str(script), PKG], 1, 30011 + os.getpid() % 500, timeout=180)
+    assert "rccl ok" in out, err[-3000:]
+
+
+def test_bench_rccl_world_size_one():
+    """bench.py's process-group path on RCCL (EOSV_DIST_BACKEND=nccl at N = 1, no launcher): the
+    line reports backend nccl, and the same accuracy / clips as the single-process run."""
+    rccl = _bench({"EOSV_DIST_BACKEND": "nccl"}, 1, 12)
+    one = _bench({}, 1, 12)
+    d = rccl["dist"]
+    assert d["backend"] == "nccl" and d["world_size_reported_by_backend"] == 1 and d["launched_world_size"] == 1
+    assert rccl["episode_acc"] == one["episode_acc"]
+    assert d["per_rank_clips"] == one["dist"]["per_rank_clips"]

@@ -154,7 +154,8 @@ def test_backbone_bf16_close_to_f32_oracle(name, res):
 
 def test_bf16_episode_agreement():
     """bf16 predictions on the C1 reference episodes: agreement with the f32 reference
-    predictions >= 90% (the bf16 acceptance rule; f32 is bit-exact)."""
+    predictions >= 97 % (the bf16 acceptance rule, r04: set to the evidence -- C2 measured 0.9985
+    over 2000 episodes and every wide fixture 1.000; f32 is bit-exact)."""
     meta, arr = load_fixture("c1_r18_protonet_seed1")
     bb = engine.Backbone("resnet18", "bf16", 224, 224, max_frames=256)
     bb.load_state_dict(synth.synth_state_dict(arch.SPECS["resnet18"], 64, 0))
@@ -162,7 +163,8 @@ def test_bf16_episode_agreement():
     dev = engine.DeviceEpisodes(b, 224, 224)
     pred, emb, _ = engine.run_episodes(bb, dev, "protonet", True)
     agree = (pred.cpu().numpy() == arr["pred"][:, 0]).mean()
-    assert agree >= 0.9, agree
+    print(f"[c1 bf16] prediction agreement {agree:.3f} over {len(meta['episodes'])} episodes")
+    assert agree >= 0.97, agree
     bb.close()
 
 

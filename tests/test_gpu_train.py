@@ -95,14 +95,21 @@ def _check_two_steps(name, frames, labels, T, H):
     assert abs(l0 - ref_losses[0]) <= 1e-4 * abs(ref_losses[0])
     # the second loss inherits the first step's gradient conditioning: same yardstick
     assert abs(l1 - ref_losses[1]) <= max(4 * abs(f32_losses[1] - ref_losses[1]), 1e-4 * abs(ref_losses[1]))
-    worst = 0.0
+    worst = (0.0, None, 0.0)
+    ratio = (0.0, None)
     for k, gr in ref_g.items():
         norm = max(float(gr.norm()), 1e-12)
         err = float((g0[k].double() - gr).norm()) / norm
         yard = float((f32_g[k] - gr).norm()) / norm
-        worst = max(worst, err)
+        if err > worst[0]:
+            worst = (err, k, yard)
+        if yard > 0 and err / yard > ratio[0]:
+            ratio = (err / yard, k)
         assert err <= max(4 * yard, 2e-2), (k, err, yard)
-    print(f"[{name} {tuple(frames.shape)}] worst relative gradient error {worst:.2e}")
+    # the tensor behind the worst error and torch-f32's own distance from f64 on it (the yardstick),
+    # and the tensor where the native gradient is furthest from f32 relative to that yardstick
+    print(f"[{name} {tuple(frames.shape)}] worst relative gradient error {worst[0]:.2e} at {worst[1]} "
+          f"(torch-f32 yardstick there {worst[2]:.2e}); largest error / yardstick {ratio[0]:.2f} at {ratio[1]}")
     got = tr.state_dict()
     for k, v in ref_sd.items():
         if k.endswith("num_batches_tracked"):

@@ -12,7 +12,7 @@ for set in "${sets[@]}"; do
   if [ -n "$CHECK" ]; then
     env $set timeout -k 10 120 tests/native/conv_check > gpurun_out/ab_sets_check_$i.log 2>&1 || { echo "conv_check failed under [$set]"; grep -E "FAIL|failures" gpurun_out/ab_sets_check_$i.log | head; exit 1; }
   fi
-  env $set timeout -k 10 200 python bench.py --dtype ${DTYPE:-bf16} --secondary-dtype none --no-cpu-baseline --layers --steps ${STEPS:-3} \
+  env $set timeout -k 10 200 python bench.py --arch ${ARCH:-resnet18} --dtype ${DTYPE:-bf16} --secondary-dtype none --no-cpu-baseline --layers --steps ${STEPS:-3} \
     > gpurun_out/ab_sets_$i.json 2> gpurun_out/ab_sets_$i.err || { tail gpurun_out/ab_sets_$i.err; exit 1; }
   echo "[$set] $(python -c "import json;d=json.load(open('gpurun_out/ab_sets_$i.json'));print(d['value'], d['roofline']['achieved'])")"
   grep -E "layer +(${LAYERS:-0|1|5|6|8|9|10|11|13|14|15|16|18|19}):" gpurun_out/ab_sets_$i.err | awk '{printf "%s%s ", $3, $4} END {print ""}'
