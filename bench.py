@@ -159,35 +159,51 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     return max(per_rank), per_rank, torch.cat(preds), prof, emb.cpu().numpy()
 
 
+def traffic_key(args):
+    """The workload a PMC traffic profile belongs to: arch, frame size and BASELINE config."""
+    return f"{args.arch}@{args.res}x{args.res}/{args.config_label}"
+
+
 def measured_traffic(dtype, key):
-    """HBM bytes per conv launch from the newest profiles/<tag>_traffic.json (written by
-    tools/prof_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-    same command); EOSV_TRAFFIC_PROFILE names a specific file.  None if there is none, it was
-    measured on another workload (key = arch@HxW), or on other kernel sources than this tree's
-    (its src_sha16 differs from eosv._lib.source_digest())."""
+    """HBM bytes per conv launch from a profiles/<tag>_traffic.json written by tools/traffic_json.py
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command at this dtype
+    (tools/gpu_traffic.sh; the figure covers exactly the timed region's conv-family launches of the
+    profiled run, the same launches its traffic_algorithmic covers).  EOSV_TRAFFIC_PROFILE names a
+    specific file, else the newest matching one.  None unless the workload key, the dtype and the
+    kernel sources (src_sha16 = eosv._lib.source_digest()) all match: counters measured on other
+    kernels are never attached."""
     import glob
-    path = os.environ.get("EOSV_TRAFFIC_PROFILE") or \
-        (sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))) or [None])[-1]
-    if not path or not os.path.exists(path):
-        return None, None
-    d = json.load(open(path))
-    if dtype not in d or d.get("key") != key:
-        return None, None
     from eosv._lib import source_digest
-    if d.get("src_sha16") != source_digest():
-        # measured on other kernels than the ones in this tree: never attach a stale figure
-        return None, None
-    return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    paths = [os.environ["EOSV_TRAFFIC_PROFILE"]] if os.environ.get("EOSV_TRAFFIC_PROFILE") else \
+        sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True)
+    digest = source_digest()
+    for path in paths:
+        if not os.path.exists(path):
+            continue
+        d = json.load(open(path))
+        if d.get("key") == key and d.get("src_sha16") == digest and dtype in d:
+            return d[dtype], os.path.relpath(path, REPO)
+    return None, None
 
 
-def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, launches, chunks):
-    """Conv-family algorithmic bytes per launch: every launch's input + output (+ residual or
-    folded-downsample input) map once per frame and its weights once per chunk
-    (arch.conv_launch_bytes: the fused stem + pool reads the f32 frame and writes the pooled map)."""
+def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, prof):
+    """Conv-family algorithmic bytes per launch over the timed region's launches: every launch's
+    input + output (+ residual or folded-downsample input) map once per frame and its weights once
+    per launch (arch.conv_launch_bytes: the fused stem + pool reads the f32 frame and writes the
+    pooled map); a bf16 conv1 fused into the previous conv3 launch (pair kernels) adds its bytes
+    less its never-read input map (as layer_bounds)."""
+    ms, fl, nl = prof
     layers = arch_mod.conv_launch_bytes(arch_mod.SPECS[args.arch], args.res, args.res, ELEM_BYTES[dtype])
-    per_frame = sum(e[0] for e in layers)
-    weights = sum(e[1] for e in layers)
-    return (frames * per_frame + chunks * weights) / launches
+    total = 0.0
+    for i in range(min(len(layers), len(nl))):
+        pf, wb, pin = layers[i]
+        if nl[i]:
+            total += frames * pf + int(nl[i]) * wb
+        elif pf:  # fused into the previous launch: same frames, its input map never read
+            j = max((k for k in range(i) if nl[k]), default=None)
+            if j is not None:
+                total += frames * (pf - pin) + int(nl[j]) * wb
+    return total / max(1, int(nl.sum()))
 
 
 def layer_bounds(prof, dtype, args, arch_mod, frames):
@@ -258,12 +274,16 @@ def roofline(prof, dtype, args=None, arch_mod=None, frames=None):
         out["kernel"] += ("; f32x3 = conv_bf16 kernels on the split (hi, lo) layout + the split-bf16 fused "
                           "stem (stem_pool_x3_cb_kernel), algorithmic (f32) FLOPs; peak = bf16 dense peak / 3")
     if args is not None and nl.sum() > 0:
-        tr, src = measured_traffic(dtype, f"{args.arch}@{args.res}x{args.res}")
-        out["traffic"] = tr
+        out["conv_launches"] = int(nl.sum())
+        out["traffic_key"] = traffic_key(args)
+        tr, src = measured_traffic(dtype, out["traffic_key"])
+        out["traffic"] = tr["hbm_bytes_per_launch"] if tr else None
         out["traffic_unit"] = "HBM bytes per conv launch"
-        out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, int(nl.sum()),
-                                                                        int(nl[0])))
+        out["traffic_algorithmic"] = round(algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, prof))
         out["traffic_source"] = src
+        if tr:  # the profiled run's own figures, over the same launches as its measured bytes
+            out["traffic_profiled_run"] = {k: tr[k] for k in ("launches", "hbm_bytes_per_launch",
+                                                               "algorithmic_bytes_per_launch", "ratio") if k in tr}
         out["per_layer_bound"] = layer_bounds(prof, dtype, args, arch_mod, frames)
     return out
 

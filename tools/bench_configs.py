@@ -23,6 +23,9 @@ PKG = os.path.join(REPO, "embodied-one-shot-video-recognition_amd")
 sys.path.insert(0, PKG)
 
 
+C3_KEY = "c3:resnet50@224x224/BASELINE configs[2]"
+
+
 def config3(args):
     import numpy as np
     import torch
@@ -74,7 +77,21 @@ def config3(args):
     if args.cpu_episodes:
         cpu, parity = c3_cpu_baseline(tn, gal, plans[:args.cpu_episodes], preds[:args.cpu_episodes])
     acc = float(np.mean([p == q["query_y"] for p, q in zip(preds, plans)]))
-    roofline["traffic"], roofline["traffic_source"] = c3_traffic(args.dtype)
+    # like-for-like traffic (tools/gpu_traffic.sh, tools/traffic_json.py): the timed region's conv
+    # launches, their algorithmic bytes per launch (bench.py's formula; frames from the stem's FLOPs)
+    sys.path.insert(0, REPO)
+    import bench as bench_mod
+    stem_flops = 2.0 * 112 * 112 * 64 * 147
+    frames_timed = int(round(float(fl[0]) / stem_flops))
+    roofline["conv_launches"] = int(nl.sum())
+    roofline["traffic_key"] = C3_KEY
+    roofline["traffic_algorithmic"] = round(bench_mod.algorithmic_bytes_per_launch(
+        argparse.Namespace(arch="resnet50", res=224), arch, args.dtype, frames_timed, (ms, fl, nl)))
+    tr, roofline["traffic_source"] = bench_mod.measured_traffic(args.dtype, C3_KEY)
+    roofline["traffic"] = tr["hbm_bytes_per_launch"] if tr else None
+    if tr:
+        roofline["traffic_profiled_run"] = {k: tr[k] for k in ("launches", "hbm_bytes_per_launch",
+                                                                "algorithmic_bytes_per_launch", "ratio") if k in tr}
     roofline["traffic_unit"] = "HBM bytes per conv launch (PMC)"
     reforward = os.environ.get("EOSV_AUG_REFORWARD", "0") == "1"
     # backbone frames per episode: query (<=16) + 5 supports x 16 (+ 40 augmented clips x 16 when
@@ -96,19 +113,6 @@ def config3(args):
             "end_to_end_tflops": round(args.episodes * frames_ep * gflop / el / 1e3, 1),
             "gallery_s": round(t_gal, 3), "gallery_frames": 10240, "episode_acc": acc,
             "roofline": roofline, "cpu_baseline": cpu, "cpu_parity": parity}
-
-
-def c3_traffic(dtype):
-    """HBM bytes per conv launch from the newest profiles/*_c3_traffic.json of this workload and
-    these kernel sources (tools/traffic_json.py over the config-3 PMC passes), else None."""
-    import glob
-
-    from eosv._lib import source_digest
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*c3*_traffic.json")), reverse=True):
-        d = json.load(open(path))
-        if d.get("key") == "c3:resnet50@224x224" and d.get("src_sha16") == source_digest() and dtype in d:
-            return d[dtype]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
-    return None, None
 
 
 def c3_cpu_baseline(tn, gal, plans, gpu_preds):

@@ -18,3 +18,8 @@ run determinism 400 python -u -m pytest -x -v --timeout 240 --timeout-method thr
 run race_r101 300 python tools/race_probe.py resnet101 bf16 8
 ARCH=resnet50 LAYERS="3|7|10|13|17|20|23|30|33|36|39" SETS="EOSV_PAIRW_CS=0;EOSV_PAIRW_CS=1;EOSV_PAIRW_CS=0;EOSV_PAIRW_CS=1" \
   timeout -k 10 600 bash tools/ab_sets.sh
+# row-strip 3x3 (conv_strip_bf16) vs the previous kernels: 0 off, 1 W >= 14, 2 also 7x7
+ARCH=resnet18 LAYERS="6|8|9|11|13|14|16|18|19" SETS="EOSV_BF16_STRIP=0;EOSV_BF16_STRIP=1;EOSV_BF16_STRIP=2;EOSV_BF16_STRIP=0;EOSV_BF16_STRIP=1;EOSV_BF16_STRIP=2" \
+  timeout -k 10 600 bash tools/ab_sets.sh
+ARCH=resnet50 LAYERS="16|19|22|29|32|35|38|41|48|51" SETS="EOSV_BF16_STRIP=0;EOSV_BF16_STRIP=1;EOSV_BF16_STRIP=2;EOSV_BF16_STRIP=0;EOSV_BF16_STRIP=1;EOSV_BF16_STRIP=2" \
+  timeout -k 10 600 bash tools/ab_sets.sh
