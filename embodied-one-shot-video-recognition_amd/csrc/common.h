@@ -149,8 +149,6 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
                          hipStream_t s, bool split = false,  // split: y in the EOSV_F32X3 (hi, lo) layout
                          LaunchInfo* info = nullptr,
                          const float* frames = nullptr);  // non-null: DIRECT (pack unused, may be null)
-bool conv_strip_bf16_ok(const ConvArgs& a);  // conv_strip_bf16.hip: stride-1 3x3, halo per strip + weight stream
-int launch_conv_strip_bf16(const ConvArgs& a, hipStream_t s);
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
 

@@ -557,10 +557,6 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
   static const int x3rows = env_switch("EOSV_X3_ROWS", 1);  // 0 = f32x3 stage-1 3x3 convs on the tap-shift kernel (A/B switch)
   if (x3rows && conv_rows_x3_ok(a)) return launch_conv_rows_x3(a, s);
-  // row-strip kernel (conv_strip_bf16.hip, r04) for the stride-1 3x3 convs of stages 2-3 (14x14 and
-  // wider maps; 7x7 maps waste 23 % of its slots: bit 1 of the switch takes them too)
-  static const int strip = env_switch("EOSV_BF16_STRIP", 0);  // 0 never, 1 W >= 14, 2 every eligible shape (A/B switch)
-  if (strip && conv_strip_bf16_ok(a) && (strip == 2 || a.W >= 14)) return launch_conv_strip_bf16(a, s);
   // tap-shift kernel (conv_bf16_ts.hip) for the stride-1 3x3 convs with Cout = 128 (r01g A/B: 5-6 %
   // faster) and the f32x3 Cout = 64 convs (512x64: 10-12 % faster than 256x64); at Cout >= 256
   // its 64-B rows lost 2-8 % to the 256x256 im2col tile
