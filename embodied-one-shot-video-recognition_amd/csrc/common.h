@@ -172,14 +172,14 @@ struct Pair1x1Args {
   // output pixel (n, oh, ow) of the Ho x Wo map
   int Ho, Wo, H2, W2;
   int abl;  // profiling-build ablation bits (EOSV_CONV_ABL), 0 otherwise
-  // pairw_bf16: elements each of x, res / y and z holds (it runs on whole PAIRW_TILE-pixel tiles)
+  // pairw_bf16: elements each of x, res / y and z holds (it runs on whole pairw_tile()-pixel rounds)
   long long cap_elems;
 };
 bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
 // pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
 // streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
-constexpr int PAIRW_TILE = 128;  // pixels per pairw round
+int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128 or 256)
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems);
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv

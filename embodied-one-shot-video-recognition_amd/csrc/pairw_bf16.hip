@@ -58,19 +58,20 @@ __device__ __forceinline__ void dma16(const unsigned char* src, void* lds) {
 }
 }  // namespace
 
-constexpr int PW_TILE = PAIRW_TILE;  // pixels per round
-
-// NPT: 16-pixel tiles per wave.  NPT = 1: 8 waves (two per SIMD); NPT = 2: 4 waves (one per SIMD,
-// 512 VGPRs) that read each LDS weight fragment once for 32 pixels -- the LDS feeds one fragment per
-// MFMA at NPT = 1, which at CMID 256 made the weight reads, not HBM, the pair's limit.
+// NPT: 16-pixel tiles per wave, 8 waves (two per SIMD); a round is 128 NPT pixels.  The LDS feeds
+// one 1-KiB weight fragment per MFMA at NPT = 1: per 64-channel chunk the 8 waves read 256 KiB
+// (stage 2) / 512 KiB (stage 3) against 1024 / 2048 MFMA cycles per SIMD, i.e. the LDS read
+// rate, not HBM, bounds the pair.  NPT = 2 (r04, the stage-2 pair with C1 = 128: 256-pixel
+// rounds, ~240 VGPRs) reads each fragment once for two pixel tiles.
 // DSC > 0 (block 0 of a stage, r03): conv3's K also holds the folded stride-2 1x1 downsample, DSC
 // more columns read from the previous stage's output x2 at pixel (2 oh, 2 ow) (ConvArgs::x2 of
 // the unfused conv), and there is no residual.
 template <int CMID, int CEXP, int C1, int NPT, int DSC = 0>
 struct PairW {
   static constexpr int K3 = CMID + DSC;                // conv3's K
-  static constexpr int NW = 8 / NPT;                   // waves per workgroup
+  static constexpr int NW = 8;                         // waves per workgroup
   static constexpr int PX = 16 * NPT;                  // pixels per wave
+  static constexpr int TILE = PX * NW;                 // pixels per round
   static constexpr int W3B = 64 * K3 * 2;  // a chunk's W3 rows (64 couts x K3), bytes
   static constexpr int W1B = C1 * 64 * 2;    // a chunk's W1 columns (C1 x 64 k), bytes
   static constexpr int STAGE_W = W3B + W1B;
@@ -97,7 +98,7 @@ struct PairW {
 // they do not drain the residual prefetch; without CS they count loads only (r03), which is
 // stricter whenever a store is still in flight.
 template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false>
-__global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a) {
+__global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   using P = PairW<CMID, CEXP, C1, NPT, DSC>;
   const int abl = ABL ? a.abl : 0;
   constexpr int K3 = P::K3, XSM = P::XSM;
@@ -111,6 +112,7 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
   const long long M = a.M;
+  constexpr int PW_TILE = P::TILE;
   const long long nrounds = (M + PW_TILE - 1) / PW_TILE;
   long long rt = blockIdx.x;  // launch: gridDim.x <= nrounds
 
@@ -417,8 +419,9 @@ __global__ __launch_bounds__(512 / NPT, 1) void pairw_bf16_kernel(Pair1x1Args a)
 template <int CMID, int CEXP, int C1, int NPT, int DSC = 0>
 static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   constexpr bool CS = EOSV_PAIRW_CS;
-  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS>, 512 / NPT);
-  const long long nrounds = (a.M + PW_TILE - 1) / PW_TILE;
+  constexpr int TILE = PairW<CMID, CEXP, C1, NPT, DSC>::TILE;
+  static const int occ = kernel_occupancy((const void*)pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS>, 512);
+  const long long nrounds = (a.M + TILE - 1) / TILE;
   if (a.plan) return record_launch(a.plan, nrounds, occ);
   const long long grid = std::min<long long>(nrounds, (long long)occ * device_cu_count());
 #ifdef EOSV_PROFILING
@@ -427,20 +430,32 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   if (abl) {
     Pair1x1Args b = a;
     b.abl = abl;
-    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, true>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, b);
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, true>), dim3((unsigned)grid), dim3(512), 0, s, b);
   } else if (cs != CS) {
-    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, !CS>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, !CS>), dim3((unsigned)grid), dim3(512), 0, s, a);
   } else
 #endif
-  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS>), dim3((unsigned)grid), dim3(512 / NPT), 0, s, a);
+  hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS>), dim3((unsigned)grid), dim3(512), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
 
+// 16-pixel tiles per wave of the pair for this shape (EOSV_PAIRW_NPT2=0 in the profiling build:
+// NPT 1 everywhere, the r03 form)
+static int pairw_npt(int cmid, int c1, int cds) {
+  // NPT 2 fits the register file only without the downsample's 8 extra X fragments (the block-0
+  // pair spills 55 VGPRs at NPT 2) and at C1 = 128 (C1 = 256: 128 accumulator VGPRs more)
+  static const int npt2 = env_switch("EOSV_PAIRW_NPT2", 1);
+  return npt2 && cmid == 128 && c1 == 128 && cds == 0 ? 2 : 1;
+}
+
+int pairw_tile(int cmid, int c1, int cds) { return 128 * pairw_npt(cmid, c1, cds); }
+
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems) {
   if (M <= 0) return false;
   // the tail round reads and writes whole tiles: x, res / y and z must hold the padded pixel count
-  const long long padded = (M + PW_TILE - 1) / PW_TILE * PW_TILE;
+  const long long tile = pairw_tile(cmid, c1, cds);
+  const long long padded = (M + tile - 1) / tile * tile;
   if (padded * std::max(cmid, std::max(cexp, c1)) > cap_elems) return false;
   if (cds) return cmid == 128 && cexp == 512 && c1 == 128 && cds == 256;  // stage-2 block 0
   return (cmid == 128 && cexp == 512 && (c1 == 128 || c1 == 256)) || (cmid == 256 && cexp == 1024 && c1 == 256);
@@ -451,7 +466,8 @@ int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
       (a.cds ? (!a.x2 || a.res || a.Ho <= 0 || a.Wo <= 0 || a.H2 < 2 * a.Ho - 1 || a.W2 < 2 * a.Wo - 1) : (!a.res || a.x2)))
     return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   if (a.cds) return launch_pairw<128, 512, 128, 1, 256>(a, s);
-  if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128, 1>(a, s);
+  if (a.cmid == 128 && a.c1 == 128)
+    return pairw_npt(128, 128, 0) == 2 ? launch_pairw<128, 512, 128, 2>(a, s) : launch_pairw<128, 512, 128, 1>(a, s);
   if (a.cmid == 128) return launch_pairw<128, 512, 256, 1>(a, s);
   return launch_pairw<256, 1024, 256, 1>(a, s);
 }

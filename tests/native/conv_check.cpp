@@ -520,7 +520,8 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   auto fill = [&](std::vector<unsigned short>& v, float scale) {
     for (auto& e : v) e = f2bf(frand(s) * scale);
   };
-  const long long Mp = (M + PAIRW_TILE - 1) / PAIRW_TILE * PAIRW_TILE;  // padded to whole rounds
+  const long long tile = pairw_tile(cmid, c1, cds);  // 128 or 256 pixels per round
+  const long long Mp = (M + tile - 1) / tile * tile;  // padded to whole rounds
   std::vector<unsigned short> x(Mp * cmid, 0x7fc0), res(Mp * cexp, 0x7fc0), w3((size_t)cexp * K3), w1((size_t)c1 * cexp);
   std::vector<unsigned short> x2(cds ? (size_t)N * H2 * W2 * cds : 1);
   {
@@ -562,7 +563,7 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   long bady = 0, badz = 0;
   double maxd = 0;
   int rcp = 0;
-  const int REPS = M % PAIRW_TILE ? 8 : 1;
+  const int REPS = M % tile ? 8 : 1;
   for (int rep = 0; rep < REPS; ++rep) {
     hipMemset(y1, 0xff, Mp * cexp * 2); hipMemset(z1, 0xff, Mp * c1 * 2);
     rcp |= launch_pairw_bf16(p, 0);
