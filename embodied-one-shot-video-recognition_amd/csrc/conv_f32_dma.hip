@@ -108,7 +108,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   }
 
   // tap of the next A stage, advanced per stage call (k0 grows by BK; Cin % BK == 0): no
-  // per-K-step divisions by Cin and KW
+  // per-K-step divisions by Cin and KW.  K order (kh, kw, cin), or with a.kcm (r04: weights
+  // stored that way) chunk-major (cin / KC, kh, kw, cin % KC): a pixel's next tap is read
+  // KC / BK K-steps later instead of Cin / BK, while its rows are still in L2
+  constexpr int KC = 32;
+  static_assert(KC % BK == 0, "a K-step stays within one channel chunk");
+  const bool kcm = a.kcm != 0;
   int nc0 = 0, nkw = 0, nkh = 0;
   auto stage = [&](int k0, int slot) {
     float* As = smem + slot * STAGE;
@@ -134,7 +139,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
       const int kh = nkh, kw = nkw;
       const long long toff = ((long long)kh * a.W + kw) * a.Cin + nc0;  // wave-uniform
       nc0 += BK;
-      if (nc0 == a.Cin) {
+      if (kcm) {
+        if ((nc0 & (KC - 1)) == 0) {  // chunk done for this tap: next tap, same chunk
+          nc0 -= KC;
+          if (++nkw == a.KW) {
+            nkw = 0;
+            if (++nkh == a.KH) nkh = 0, nc0 += KC;  // all taps done: next chunk
+          }
+        }
+      } else if (nc0 == a.Cin) {
         nc0 = 0;
         if (++nkw == a.KW) nkw = 0, ++nkh;
       }
@@ -171,8 +184,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   const int kb = (int)((long long)nkt * blockIdx.y / gridDim.y);
   const int nk = (int)((long long)nkt * (blockIdx.y + 1) / gridDim.y) - kb;
   if (kb > 0 && !STEM) {  // the tap counters of K column kb * BK
-    const int k = kb * BK, t = k / a.Cin;
-    nc0 = k - t * a.Cin;
+    const int k = kb * BK;
+    int t;
+    if (kcm) {
+      const int per = KC * a.KH * a.KW, ch = k / per, rem = k - ch * per;
+      t = rem / KC;
+      nc0 = ch * KC + (rem - t * KC);
+    } else {
+      t = k / a.Cin;
+      nc0 = k - t * a.Cin;
+    }
     nkh = t / a.KW;
     nkw = t - nkh * a.KW;
   }
@@ -397,7 +418,7 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
   if (stem) return launch_dma<128, 64, 16, 2, 2, true>(a, s);
   // stage-1 3x3 64->64 convs: row-strip direct conv (input staged once per strip, not per tap)
   static const int rows = env_switch("EOSV_F32_ROWS", 1);  // 0 = implicit GEMM (A/B switch)
-  if (rows && conv_rows_f32_ok(a)) return launch_conv_rows_f32(a, s);
+  if (rows && !a.kcm && conv_rows_f32_ok(a)) return launch_conv_rows_f32(a, s);
   if (a.Cout % 4) {
     if (a.x2) return set_error("conv_f32: fused downsample needs Cout % 4 == 0"), EOSV_ERR_UNSUPPORTED;
     return launch_dma<128, 64, 16, 2, 2, false, 2, false>(a, s);

@@ -49,7 +49,8 @@ int env_switch(const char* name, int dflt) {
 struct Conv {
   int cin = 0, cout = 0, kh = 1, kw = 1, kwp = 1, cinp = 0, stride = 1, pad = 0, K = 0;
   bool stem = false;
-  bool kcm = false;           // bf16 weights in chunk-major K order (ConvArgs::kcm)
+  bool kcm = false;           // weights in chunk-major K order (ConvArgs::kcm), chunks of kcmc channels
+  int kcmc = 64;
   int kds = 0;                // fused downsample: extra K columns (its Cin) after this conv's K
   int id = 0;                 // layer id for profiling (plan order)
   std::string wname, bnname;  // state_dict prefixes
@@ -337,13 +338,20 @@ static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::ve
     for (int o = 0; o < c.cout; ++o) beta[o] = bias[o];
   }
   // bf16 multi-tap convs with Cin > 64: K chunk-major, (cin / 64, kh, kw, cin % 64), so that a
-  // conv's K walk visits all taps of one 64-channel slice of the input before the next slice
-  // (conv_bf16_p8.hip)
-  c.kcm = bf16 && !c.stem && c.cinp % 64 == 0 && c.cinp > 64 && c.kh * c.kw > 1 && c.kwp == c.kw;
+  // conv's K walk visits all taps of one 64-channel slice of the input before the next slice.
+  // f32 multi-tap convs with Cin >= 128 (the implicit GEMM's; stage 1 takes the row kernel):
+  // (cin / 32, kh, kw, cin % 32), r04: in tap-major order a pixel's next tap came Cin / 16 K-steps
+  // later, when the XCD's 64 workgroups had staged ~8 MB and L2 (4 MB) had turned over, so the
+  // tap re-reads came from beyond L2 (PMC r03: 3.6x the algorithmic bytes); chunk-major brings
+  // them 2 K-steps later, and the two 64-B halves of a 128-B pixel line in consecutive K-steps
+  static const int f32kcm = env_switch("EOSV_F32_KCM", 1);  // 0 = tap-major (A/B switch)
+  c.kcmc = bf16 ? 64 : 32;
+  c.kcm = !c.stem && c.cinp % c.kcmc == 0 && c.kh * c.kw > 1 && c.kwp == c.kw &&
+          (bf16 ? c.cinp > 64 : (f32kcm && c.cinp >= 128));
   wf.assign((size_t)c.cout * c.K, 0.f);
   if (split && c.cinp != 3 * c.cin) return set_error("fold_conv: split layout needs 3 * cin channels"), false;
   auto kidx = [&](int i, int y, int x) {
-    return c.kcm ? ((size_t)(i / 64) * c.kh * c.kw + y * c.kw + x) * 64 + i % 64
+    return c.kcm ? ((size_t)(i / c.kcmc) * c.kh * c.kw + y * c.kw + x) * c.kcmc + i % c.kcmc
                  : ((size_t)y * c.kwp + x) * c.cinp + i;
   };
   for (int o = 0; o < c.cout; ++o)

@@ -15,8 +15,9 @@ static float frand(unsigned& s) { s = s * 1664525u + 1013904223u; return ((s >> 
 // ds_cin > 0: a fused 1x1 stride-2 downsample (ConvArgs::x2) reads x2 [N][2H][2W][ds_cin] into K
 // columns [K1, K1 + ds_cin).  tol: bound on |err| / (1 + sum of |terms|) -- f32 rounding of a
 // K-term dot product grows with the magnitudes summed, not with the (cancelling) result.
+// kcm: device weights in the chunk-major K order (cin / 32, kh, kw, cin % 32) (ConvArgs::kcm, f32)
 static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int pad, bool stem, bool res, bool relu,
-                 int ds_cin = 0, double tol = 1e-5) {
+                 int ds_cin = 0, double tol = 1e-5, bool kcm = false) {
   // stem: dense padded RGB input [N][H+2p][Wp][3] (zero borders), K = [kh][24] padded to 16
   const int KWp = stem ? 8 : K, Cinp = Cin;
   const int Ho = (H + 2 * pad - K) / stride + 1, Wo = (W + 2 * pad - K) / stride + 1;
@@ -50,10 +51,17 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
   hipMalloc(&dx, x.size() * 4); hipMalloc(&dw, w.size() * 4); hipMalloc(&db, b.size() * 4);
   hipMalloc(&dr, r.size() * 4); hipMalloc(&dy, r.size() * 4);
   hipMemcpy(dx, x.data(), x.size() * 4, hipMemcpyHostToDevice);
-  hipMemcpy(dw, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  std::vector<float> wd = w;
+  if (kcm)
+    for (int o = 0; o < Cout; ++o)
+      for (int t = 0; t < K * K; ++t)
+        for (int c = 0; c < Cin; ++c)
+          wd[(size_t)o * Kd + ((c / 32) * K * K + t) * 32 + c % 32] = w[(size_t)o * Kd + t * Cinp + c];
+  hipMemcpy(dw, wd.data(), wd.size() * 4, hipMemcpyHostToDevice);
   hipMemcpy(db, b.data(), b.size() * 4, hipMemcpyHostToDevice);
   hipMemcpy(dr, r.data(), r.size() * 4, hipMemcpyHostToDevice);
   ConvArgs a{};
+  a.kcm = kcm;
   a.x = dx; a.w = dw; a.bias = db; a.res = res ? dr : nullptr; a.y = dy;
   a.N = N; a.H = H; a.W = W; a.Cin = Cinp; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KH = K; a.KW = K; a.KWp = KWp; a.stride = stride; a.pad = pad; a.K = Kd; a.relu = relu;
@@ -94,8 +102,8 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
           if (!(e <= tol * (1 + sabs))) { if (bad < 5) printf("  bad n%d oh%d ow%d o%d ref %f got %f\n", n, oh, ow, o, acc, y[oi]); ++bad; }
           maxerr = fmax(maxerr, e); maxref = fmax(maxref, fabs(acc));
         }
-  printf("%s f32 N%d H%d W%d Cin%d Cout%d K%d s%d p%d res%d relu%d ds%d rc=%d maxerr %.3e (maxref %.3e) bad %ld\n",
-         bad || rc ? "FAIL" : "ok  ", N, H, W, Cin, Cout, K, stride, pad, res, relu, ds_cin, rc, maxerr, maxref, bad);
+  printf("%s f32 N%d H%d W%d Cin%d Cout%d K%d s%d p%d res%d relu%d ds%d kcm%d rc=%d maxerr %.3e (maxref %.3e) bad %ld\n",
+         bad || rc ? "FAIL" : "ok  ", N, H, W, Cin, Cout, K, stride, pad, res, relu, ds_cin, kcm, rc, maxerr, maxref, bad);
   hipFree(dx); hipFree(dw); hipFree(db); hipFree(dr); hipFree(dy);
   if (dx2) hipFree(dx2);
   hipFree(dz);
@@ -686,6 +694,15 @@ int main() {
   fails += check(6, 14, 14, 256, 256, 3, 1, 1, false, true, true, 0, 2e-6);
   fails += check(4, 14, 14, 256, 256, 3, 1, 1, false, false, true, 128, 2e-6);
   fails += check(3, 7, 7, 512, 512, 3, 1, 1, false, false, true, 256, 2e-6);
+  // chunk-major K order (r04, the library's f32 weights at Cin >= 128): the R18 / R50 stage-2..4
+  // 3x3s at grids that take every tile (256x128, 128x128, 128x64), stride 2, the fused downsample
+  fails += check(50, 28, 28, 128, 128, 3, 1, 1, false, true, true, 0, 2e-6, true);
+  fails += check(40, 28, 28, 128, 128, 3, 1, 1, false, false, true, 64, 2e-6, true);
+  fails += check(60, 14, 14, 256, 256, 3, 1, 1, false, true, true, 0, 2e-6, true);
+  fails += check(30, 28, 28, 128, 256, 3, 2, 1, false, false, true, 0, 2e-6, true);
+  fails += check(40, 7, 7, 512, 512, 3, 1, 1, false, true, true, 0, 2e-6, true);
+  fails += check(4, 14, 14, 256, 256, 3, 1, 1, false, false, true, 128, 2e-6, true);
+  fails += check(3, 9, 11, 160, 96, 3, 1, 1, false, true, false, 0, 2e-6, true);
   // grids at / above the CU count: the large 256x128 and 128x128 tiles (small N takes 128x64)
   fails += check(21, 56, 56, 32, 128, 3, 1, 1, false, true, true, 0, 2e-6);
   fails += check(11, 28, 28, 32, 512, 1, 1, 0, false, false, true, 0, 2e-6);

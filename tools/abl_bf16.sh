@@ -5,7 +5,7 @@ export EOSV_LIBRARY="${EOSV_LIBRARY:-$PWD/embodied-one-shot-video-recognition_am
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for abl in ${ABLS:-0 1 4 8 2}; do
-  EOSV_CONV_ABL=$abl timeout -k 10 300 python bench.py --dtype bf16 --secondary-dtype none --steps 3 --warmup 1 \
+  EOSV_CONV_ABL=$abl timeout -k 10 300 python bench.py --arch ${ARCH:-resnet18} --dtype bf16 --secondary-dtype none --steps 3 --warmup 1 \
     --no-cpu-baseline --layers > gpurun_out/ablb_$abl.log 2>&1 || { tail gpurun_out/ablb_$abl.log; exit 1; }
   echo "abl $abl: $(grep -o '"achieved": [0-9.]*' gpurun_out/ablb_$abl.log)"
 done
