@@ -508,7 +508,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 // slot kt.  12 waves = 3 per SIMD: every wave gets <= 168 VGPRs, so the consumers keep one set of
 // B fragments (the 256x256 kernel's double-buffered B set alone is 32 VGPRs more).  Producers
 // leave after the K loop (s_barrier then waits only for the surviving consumer waves).
-template <int BM, int BN, int WM, int WN, int NP>
+// NSA = 3 (EOSV_BF16_WS=2): split rings as conv_bf16_kernel's NSA: 3 A slots (the im2col rows, staged
+// two K-steps ahead) and 2 B slots (the weights, one ahead), 160 KiB.
+template <int BM, int BN, int WM, int WN, int NP, int NSA = 0>
 __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvArgs a) {
   constexpr int BK = 64, CPR = 8, RPP = 8, MF = 16, KS = 32;
   constexpr int NW = WM * WN;
@@ -516,7 +518,12 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
   constexpr int AI = BM / (RPP * NP), BI = BN / (RPP * NP);  // DMA pieces per producer wave per stage
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(AI >= 1 && BI >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * STAGE];
+  static_assert(NSA == 0 || NSA == 3, "one ring, or 3 A + 2 B slots");
+  constexpr int SMEM = NSA ? NSA * BM * BK + 2 * BN * BK : 2 * STAGE;
+  __shared__ __attribute__((aligned(16))) u16 smem[SMEM];
+  // A slot of K-step kt, B slot of K-step kt
+  auto a_slot = [&](int kt) { return NSA ? smem + (kt % (NSA ? NSA : 1)) * BM * BK : smem + (kt & 1) * STAGE; };
+  auto b_slot = [&](int kt) { return NSA ? smem + NSA * BM * BK + (kt & 1) * BN * BK : smem + (kt & 1) * STAGE + BM * BK; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -562,9 +569,12 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
       const int n = n0 + row;
       brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 8 : nullptr;
     }
-    auto stage = [&](int k0, int slot) {
-      u16* As = smem + slot * STAGE;
-      u16* Bs = As + BM * BK;
+    // skip 4: no A rows, 8: no B rows
+    auto stage = [&](int kt, int skip) {
+      const int k0 = kt * BK;
+      u16* As = a_slot(kt);
+      u16* Bs = b_slot(kt);
+      if (!(skip & 4)) {
       int tap, c0;
       ktap(a, k0, tap, c0);
       const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
@@ -577,6 +587,8 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
         u16* dst = As + (pw * (BM / NP) + RPP * j) * BK;
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
+      }
+      if (skip & 8) return;
       const int kb = wcol(a, k0);
 #pragma unroll
       for (int j = 0; j < BI; ++j) {
@@ -585,12 +597,33 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     };
-    if (nk > 0) stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (NSA) {  // B(0), A(0), then A(1) may stay in flight
+      if (nk > 0) stage(0, 0);
+      if (nk > 1) {
+        stage(1, 8);
+        vm_wait<AI>();
+      } else {
+        vm_wait<0>();
+      }
+    } else {
+      if (nk > 0) stage(0, 0);
+      vm_wait<0>();
+    }
     __builtin_amdgcn_s_barrier();
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk && !(EOSV_ABL(a) & 1)) stage((kt + 1) * BK, (kt + 1) & 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NSA) {  // B(kt + 1), then A(kt + 2); B(kt + 1) and A(kt + 1) must land, A(kt + 2) may fly
+        if (!(EOSV_ABL(a) & 1)) {
+          if (kt + 1 < nk) stage(kt + 1, 4);
+          if (kt + 2 < nk) stage(kt + 2, 8);
+        }
+        if (kt + 2 < nk)
+          vm_wait<AI>();
+        else
+          vm_wait<0>();
+      } else {
+        if (kt + 1 < nk && !(EOSV_ABL(a) & 1)) stage(kt + 1, 0);
+        vm_wait<0>();
+      }
       __builtin_amdgcn_s_barrier();
     }
     return;
@@ -610,8 +643,8 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
   __builtin_amdgcn_s_barrier();  // stage 0 has landed
   asm volatile("" ::: "memory");
   for (int kt = 0; kt < nk; ++kt) {
-    const u16* As = smem + (kt & 1) * STAGE;
-    const u16* Bs = As + BM * BK;
+    const u16* As = a_slot(kt);
+    const u16* Bs = b_slot(kt);
     if (!(EOSV_ABL(a) & (16 | 32))) {
       // groups (slice s, A row tile i) of TN MFMAs; the next group's A fragment is read while this
       // group's MFMAs run, the slice's B fragments at its first group
@@ -655,7 +688,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
   u16* __restrict__ y = (u16*)a.y;
   const u16* __restrict__ res = (const u16*)a.res;
   constexpr int EPR = WM * 32, EPS = BN + 4;
-  static_assert(EPR * EPS * 4 <= 2 * STAGE * 2, "epilogue tile must fit the ring");
+  static_assert(EPR * EPS * 4 <= SMEM * 2, "epilogue tile must fit the ring");
   float* ep = (float*)smem;
   float bcol[TN];
 #pragma unroll
@@ -739,20 +772,21 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
 }
 
 static int bf16_ws() {
-  static const int v = env_switch("EOSV_BF16_WS", 0);  // 1 = warp-specialised 256x256 tile on the stride-1 3x3s (A/B switch)
+  static const int v = env_switch("EOSV_BF16_WS", 0);  // warp-specialised 256x256 tile on the stride-1 3x3s: 1 one ring, 2 split rings (A/B switch)
   return v;
 }
 
+template <int NSA>
 static int launch_bf16_ws(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NP = 4;
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
   if (a.plan) {
-    static const int occ = kernel_occupancy((const void*)conv_bf16_ws_kernel<BM, BN, WM, WN, NP>, 64 * (WM * WN + NP));
+    static const int occ = kernel_occupancy((const void*)conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA>, 64 * (WM * WN + NP));
     return record_launch(a.plan, nb, occ);
   }
-  hipLaunchKernelGGL((conv_bf16_ws_kernel<BM, BN, WM, WN, NP>), dim3((unsigned)nb), dim3(64 * (WM * WN + NP)), 0, s, a);
+  hipLaunchKernelGGL((conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA>), dim3((unsigned)nb), dim3(64 * (WM * WN + NP)), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -850,7 +884,7 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     if constexpr (EOSV_BF16_ARING != 0)
       if (EOSV_BF16_ARING == 2 || a.KH * a.KW == 1 || a.stride != 1 || a.x2)
         return launch_bf16<256, 256, 2, 4, false, 2, 64, 3>(a, s);
-    if (bf16_ws() && !a.split && !a.x2) return launch_bf16_ws(a, s);
+    if (bf16_ws() && !a.split && !a.x2) return bf16_ws() == 2 ? launch_bf16_ws<3>(a, s) : launch_bf16_ws<0>(a, s);
     return launch_bf16<256, 256, 2, 4, false>(a, s);
   }
   return launch_bf16<128, 64, 2, 2, false>(a, s);
