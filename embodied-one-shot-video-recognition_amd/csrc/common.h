@@ -88,8 +88,8 @@ struct ConvArgs {
   const void* zero;   // >= 64 zeroed bytes (DMA target for out-of-bounds taps)
   int abl;            // ablation bits for profiling builds (0 = normal)
   int xcd;            // 1: XCD-aware block order (each XCD walks a contiguous range of tiles)
-  int kcm;            // K chunk-major: (cin/64, kh, kw, cin%64) for bf16, (cin/32, kh, kw, cin%32) for f32,
-                      // instead of (kh, kw, cin)
+  int kcm;            // K chunk-major instead of (kh, kw, cin): bf16 nonzero = (cin/64, kh, kw, cin%64);
+                      // f32 = the chunk C, (cin/C, kh, kw, cin%C)
   // fused 1x1 downsample (ResNet block shortcut): K columns [K1, K) read x2 at output pixel
   // (oh, ow) -> x2 pixel (oh * stride2, ow * stride2), channel k - K1; nullptr = none
   const void* x2;     // NHWC [N, H2, W2, Cin2]

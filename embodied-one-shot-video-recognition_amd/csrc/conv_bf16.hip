@@ -508,9 +508,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 // slot kt.  12 waves = 3 per SIMD: every wave gets <= 168 VGPRs, so the consumers keep one set of
 // B fragments (the 256x256 kernel's double-buffered B set alone is 32 VGPRs more).  Producers
 // leave after the K loop (s_barrier then waits only for the surviving consumer waves).
-// NSA = 3 (EOSV_BF16_WS=2): split rings as conv_bf16_kernel's NSA: 3 A slots (the im2col rows, staged
-// two K-steps ahead) and 2 B slots (the weights, one ahead), 160 KiB.
-template <int BM, int BN, int WM, int WN, int NP, int NSA = 0>
+// NSA = 3: split rings as conv_bf16_kernel's NSA: 3 A slots (the im2col rows, staged two K-steps
+// ahead) and 2 B slots (the weights, one ahead), 160 KiB (256x256 tiles; r04 A/B on the stride-1
+// 3x3s: one ring 6-7 %, split rings 13 % faster than conv_bf16_kernel's one ring).  DS / SPLIT as in
+// conv_bf16_kernel (the folded downsample's K columns; the f32x3 split layout).
+template <int BM, int BN, int WM, int WN, int NP, int NSA, bool DS, bool SPLIT>
 __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvArgs a) {
   constexpr int BK = 64, CPR = 8, RPP = 8, MF = 16, KS = 32;
   constexpr int NW = WM * WN;
@@ -544,6 +546,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
     const u16* zero = (const u16*)a.zero;
     const int lr = lane / CPR, pc = lane & (CPR - 1);
     const u16* arow[AI];
+    const u16* arow2[DS ? AI : 1];  // DS: the fused downsample's input pixel (always in bounds)
     int aih[AI], aiw[AI];
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
@@ -555,10 +558,13 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
         aih[j] = oh * a.stride - a.pad;
         aiw[j] = ow * a.stride - a.pad;
         arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.xs + lc * 8;
+        if constexpr (DS)
+          arow2[j] = (const u16*)a.x2 + (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.x2s + lc * 8;
       } else {
         aih[j] = -(1 << 28);
         aiw[j] = 0;
         arow[j] = x;
+        if constexpr (DS) arow2[j] = nullptr;
       }
     }
     const u16* brow[BI];
@@ -574,19 +580,27 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
       const int k0 = kt * BK;
       u16* As = a_slot(kt);
       u16* Bs = b_slot(kt);
-      if (!(skip & 4)) {
-      int tap, c0;
-      ktap(a, k0, tap, c0);
-      const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
-      const long long toff = ((long long)kh * a.W + kw) * a.xs + c0;
+      if (skip & 4) {
+      } else if (DS && k0 >= a.K1) {
 #pragma unroll
-      for (int j = 0; j < AI; ++j) {
-        const int ih = aih[j] + kh, iw = aiw[j] + kw;
-        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        const u16* src = ok ? arow[j] + toff : zero;
-        u16* dst = As + (pw * (BM / NP) + RPP * j) * BK;
-        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-      }
+        for (int j = 0; j < (DS ? AI : 1); ++j) {
+          const u16* src = arow2[j] ? arow2[j] + (SPLIT ? split_chan(k0 - a.K1, a.Cin2) : k0 - a.K1) : zero;
+          u16* dst = As + (pw * (BM / NP) + RPP * j) * BK;
+          __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+      } else {
+        int tap, c0;
+        ktap(a, k0, tap, c0);
+        const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+        const long long toff = ((long long)kh * a.W + kw) * a.xs + (SPLIT ? split_chan(c0, a.Cin) : c0);
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+          const int ih = aih[j] + kh, iw = aiw[j] + kw;
+          const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+          const u16* src = ok ? arow[j] + toff : zero;
+          u16* dst = As + (pw * (BM / NP) + RPP * j) * BK;
+          __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
       }
       if (skip & 8) return;
       const int kb = wcol(a, k0);
@@ -700,7 +714,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
   constexpr int TPP = 32 / MF, NPASS = BM / WM / 32;
   constexpr int IPT = EPR * (BN / 8) / (64 * NW);
   static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
-  const long long ostr = a.Cout;
+  const long long ostr = SPLIT ? 2LL * a.Cout : a.Cout;  // output / residual pixel stride
   const long long tile_bytes = (long long)min(BM, M - m0) * ostr * 2;
   const int nrec = (int)min(tile_bytes, 0x7fffffffLL);
   const __amdgpu_buffer_rsrc_t yr =
@@ -708,7 +722,11 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(res ? res + (long long)m0 * ostr : (const u16*)a.zero), (short)0, res ? nrec : 0, 0x00020000);
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  v4u rv[2][IPT];
+  // residual sets: two (pass i + 1's loads in flight during pass i), one with SPLIT (its lo block
+  // doubles them: two sets spilled 38 VGPRs; pass i's then load at its start, under the LDS write)
+  constexpr int NRB = SPLIT ? 1 : 2;
+  v4u rv[NRB][IPT];
+  v4u rl[NRB][SPLIT ? IPT : 1];  // SPLIT: the residual's lo block
   auto chunk = [&](int i, int t, int& lrow, int& c8, int& voff) {
     const int idx = tid + t * nthreads;
     lrow = idx / (BN / 8);
@@ -722,18 +740,20 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
     for (int t = 0; t < IPT; ++t) {
       int lrow, c8, voff;
       chunk(i, t, lrow, c8, voff);
-      rv[i & 1][t] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, 0, 0);
+      rv[i % NRB][t] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, 0, 0);
+      if constexpr (SPLIT) rl[i % NRB][SPLIT ? t : 0] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff + 2 * a.Cout, 0, 0);
     }
   };
   // the residual of pass i + 1 is loaded once pass i's accumulators are in LDS (their registers
   // are dead by then): with the 168-VGPR budget of 12 waves, holding two residual sets beside all
   // 128 accumulators spilled
-  load_res(0);
+  if constexpr (!SPLIT) load_res(0);
   const float rlow = a.relu ? 0.f : -INFINITY;
 #pragma unroll
   for (int i = 0; i < NPASS; ++i) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if constexpr (SPLIT) load_res(i);
 #pragma unroll
     for (int t = 0; t < TPP; ++t)
 #pragma unroll
@@ -745,7 +765,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
         }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (i + 1 < NPASS) load_res(i + 1);
+    if (!SPLIT && i + 1 < NPASS) load_res(i + 1);
 #pragma unroll
     for (int t = 0; t < IPT; ++t) {
       int lrow, c8, voff;
@@ -753,40 +773,66 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
       const float4 v0 = *(const float4*)(ep + lrow * EPS + c8 * 8);
       const float4 v1 = *(const float4*)(ep + lrow * EPS + c8 * 8 + 4);
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const v4u r4 = rv[i & 1][t];
+      const v4u r4 = rv[i % NRB][t];
       const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
+      if constexpr (SPLIT) {
+        const v4u l4 = rl[i % NRB][SPLIT ? t : 0];
+        const unsigned rlo[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff));
-        v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16));
+        for (int k = 0; k < 4; ++k) {  // hi + lo is exact in f32
+          v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff)) + bf_to_f((u16)(rlo[k] & 0xffff));
+          v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16)) + bf_to_f((u16)(rlo[k] >> 16));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += bf_to_f((u16)(ru[k] & 0xffff));
+          v[2 * k + 1] += bf_to_f((u16)(ru[k] >> 16));
+        }
       }
-      v4u pk;
+      v4u pk, pl;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const u16 blo = f_to_bf(fmaxf(v[2 * k], rlow)), bhi = f_to_bf(fmaxf(v[2 * k + 1], rlow));
+        const float lo = fmaxf(v[2 * k], rlow), hi = fmaxf(v[2 * k + 1], rlow);
+        const u16 blo = f_to_bf(lo), bhi = f_to_bf(hi);
         pk[k] = (unsigned)blo | ((unsigned)bhi << 16);
+        if constexpr (SPLIT)  // residual parts (exact differences)
+          pl[k] = (unsigned)f_to_bf(lo - bf_to_f(blo)) | ((unsigned)f_to_bf(hi - bf_to_f(bhi)) << 16);
       }
       __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff, 0, 0);
+      if constexpr (SPLIT) __builtin_amdgcn_raw_buffer_store_b128(pl, yr, voff + 2 * a.Cout, 0, 0);
     }
   }
 }
 
+// EOSV_BF16_WS bits (bf16 layout only): 1 stride-1 multi-tap convs on 256x256 tiles (split
+// rings), 2 the other 256x256 convs (1x1, stride 2, folded downsample; split rings), 4 the 512x128
+// tiles (one ring).
 static int bf16_ws() {
-  static const int v = env_switch("EOSV_BF16_WS", 0);  // warp-specialised 256x256 tile on the stride-1 3x3s: 1 one ring, 2 split rings (A/B switch)
+  static const int v = env_switch("EOSV_BF16_WS", 1);  // (A/B switch)
   return v;
 }
 
-template <int NSA>
+template <int BM, int BN, int WM, int WN, int NSA>
 static int launch_bf16_ws(const ConvArgs& a, hipStream_t s) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NP = 4;
+  constexpr int NP = 4, NT = 64 * (WM * WN + NP);
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
   if (a.plan) {
-    static const int occ = kernel_occupancy((const void*)conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA>, 64 * (WM * WN + NP));
+    static const int occ = kernel_occupancy((const void*)conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA, false, false>, NT);
     return record_launch(a.plan, nb, occ);
   }
-  hipLaunchKernelGGL((conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA>), dim3((unsigned)nb), dim3(64 * (WM * WN + NP)), 0, s, a);
+  if (a.x2 && (a.K1 % 64 || a.Cin2 % 64)) return set_error("conv_bf16: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
+  // f32x3 (split layout) stays on conv_bf16_kernel: its two residual blocks beside the 128
+  // accumulators spill 13-18 VGPRs at the 168 of 12 waves
+  if (a.split) return set_error("conv_bf16_ws: split layout"), EOSV_ERR_UNSUPPORTED;
+  const dim3 g((unsigned)nb), b(NT);
+  if (a.x2) {
+    hipLaunchKernelGGL((conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA, true, false>), g, b, 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_bf16_ws_kernel<BM, BN, WM, WN, NP, NSA, false, false>), g, b, 0, s, a);
+  }
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -875,8 +921,15 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return launch_bf16<256, 128, 2, 2, false>(a, s);
   }
 #endif
-  if (a.Cout == 128) return launch_bf16<512, 128, 4, 2, false>(a, s);
+  const int ws = a.split ? 0 : bf16_ws();  // WS classes for this conv
+  if (a.Cout == 128) {
+    if (ws & 4) return launch_bf16_ws<512, 128, 4, 2, 0>(a, s);
+    return launch_bf16<512, 128, 4, 2, false>(a, s);
+  }
   if (a.Cout >= 256) {
+    const bool s1 = a.KH * a.KW > 1 && a.stride == 1 && !a.x2;  // stride-1 multi-tap: one ring below
+    if ((ws & 1) && s1) return launch_bf16_ws<256, 256, 2, 4, 3>(a, s);
+    if ((ws & 2) && !s1) return launch_bf16_ws<256, 256, 2, 4, 3>(a, s);
     // split rings (A two K-steps ahead) for the 1x1s, the stride-2 3x3s and the fused-downsample
     // convs; the stride-1 3x3s keep the one ring (r03 A/B, ms per 3200 frames, R50: 1x1s 6-11 %
     // faster, e.g. stage-4 conv1 0.33 -> 0.29, 1x1 + downsample 1.15 -> 1.08, stride-2 3x3 0.67 ->
@@ -884,7 +937,6 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     if constexpr (EOSV_BF16_ARING != 0)
       if (EOSV_BF16_ARING == 2 || a.KH * a.KW == 1 || a.stride != 1 || a.x2)
         return launch_bf16<256, 256, 2, 4, false, 2, 64, 3>(a, s);
-    if (bf16_ws() && !a.split && !a.x2) return bf16_ws() == 2 ? launch_bf16_ws<3>(a, s) : launch_bf16_ws<0>(a, s);
     return launch_bf16<256, 256, 2, 4, false>(a, s);
   }
   return launch_bf16<128, 64, 2, 2, false>(a, s);

@@ -111,9 +111,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   // per-K-step divisions by Cin and KW.  K order (kh, kw, cin), or with a.kcm (r04: weights
   // stored that way) chunk-major (cin / KC, kh, kw, cin % KC): a pixel's next tap is read
   // KC / BK K-steps later instead of Cin / BK, while its rows are still in L2
-  constexpr int KC = 32;
-  static_assert(KC % BK == 0, "a K-step stays within one channel chunk");
-  const bool kcm = a.kcm != 0;
+  const int KC = a.kcm;  // channel chunk (a power of two, a multiple of BK: the launcher checks)
+  const bool kcm = KC != 0;
   int nc0 = 0, nkw = 0, nkh = 0;
   auto stage = [&](int k0, int slot) {
     float* As = smem + slot * STAGE;
@@ -416,6 +415,8 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_dma<128, 64, 16, 2, 2, true>(a, s);
+  if (a.kcm && (a.kcm < 32 || (a.kcm & (a.kcm - 1)) || a.Cin % a.kcm))
+    return set_error("conv_f32: chunk-major K needs a power-of-two chunk >= 32 dividing Cin"), EOSV_ERR_UNSUPPORTED;
   // stage-1 3x3 64->64 convs: row-strip direct conv (input staged once per strip, not per tap)
   static const int rows = env_switch("EOSV_F32_ROWS", 1);  // 0 = implicit GEMM (A/B switch)
   if (rows && !a.kcm && conv_rows_f32_ok(a)) return launch_conv_rows_f32(a, s);

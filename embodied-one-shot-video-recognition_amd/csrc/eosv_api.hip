@@ -344,10 +344,10 @@ static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::ve
   // later, when the XCD's 64 workgroups had staged ~8 MB and L2 (4 MB) had turned over, so the
   // tap re-reads came from beyond L2 (PMC r03: 3.6x the algorithmic bytes); chunk-major brings
   // them 2 K-steps later, and the two 64-B halves of a 128-B pixel line in consecutive K-steps
-  static const int f32kcm = env_switch("EOSV_F32_KCM", 1);  // 0 = tap-major (A/B switch)
-  c.kcmc = bf16 ? 64 : 32;
-  c.kcm = !c.stem && c.cinp % c.kcmc == 0 && c.kh * c.kw > 1 && c.kwp == c.kw &&
-          (bf16 ? c.cinp > 64 : (f32kcm && c.cinp >= 128));
+  static const int f32kcm = env_switch("EOSV_F32_KCM", 32);  // f32 channel chunk; 0 = tap-major (A/B switch)
+  c.kcmc = bf16 ? 64 : f32kcm;
+  c.kcm = !c.stem && c.kcmc > 0 && c.cinp % c.kcmc == 0 && c.kh * c.kw > 1 && c.kwp == c.kw &&
+          (bf16 ? c.cinp > 64 : c.cinp >= 128);
   wf.assign((size_t)c.cout * c.K, 0.f);
   if (split && c.cinp != 3 * c.cin) return set_error("fold_conv: split layout needs 3 * cin channels"), false;
   auto kidx = [&](int i, int y, int x) {
@@ -454,7 +454,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
   a.zero = h->zero;
   static const int xcd = env_switch("EOSV_XCD", 1);  // 0 = plain blockIdx order (A/B switch)
   a.xcd = xcd;
-  a.kcm = c.kcm ? 1 : 0;
+  a.kcm = c.kcm ? (bf16 ? 1 : c.kcmc) : 0;  // bf16 kernels: a flag (64-channel chunks); f32: the chunk
   a.split = (bf16 && x3(h)) ? 1 : 0;
   a.xs = a.split ? 2 * c.cin : c.cinp;  // physical pixel strides (the split layout stores hi, lo)
   a.x2s = x2 ? (a.split ? 2 * (c.kds / 3) : c.kds) : 0;

@@ -61,7 +61,7 @@ static int check(int N, int H, int W, int Cin, int Cout, int K, int stride, int 
   hipMemcpy(db, b.data(), b.size() * 4, hipMemcpyHostToDevice);
   hipMemcpy(dr, r.data(), r.size() * 4, hipMemcpyHostToDevice);
   ConvArgs a{};
-  a.kcm = kcm;
+  a.kcm = kcm ? 32 : 0;
   a.x = dx; a.w = dw; a.bias = db; a.res = res ? dr : nullptr; a.y = dy;
   a.N = N; a.H = H; a.W = W; a.Cin = Cinp; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KH = K; a.KW = K; a.KWp = KWp; a.stride = stride; a.pad = pad; a.K = Kd; a.relu = relu;
