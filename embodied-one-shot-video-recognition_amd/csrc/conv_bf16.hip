@@ -809,7 +809,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
 // rings), 2 the other 256x256 convs (1x1, stride 2, folded downsample; split rings), 4 the 512x128
 // tiles (one ring).
 static int bf16_ws() {
-  static const int v = env_switch("EOSV_BF16_WS", 1);  // (A/B switch)
+  static const int v = env_switch("EOSV_BF16_WS", 7);  // (A/B switch)
   return v;
 }
 
