@@ -624,6 +624,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
       vm_wait<0>();
     }
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     for (int kt = 0; kt < nk; ++kt) {
       if constexpr (NSA) {  // B(kt + 1), then A(kt + 2); B(kt + 1) and A(kt + 1) must land, A(kt + 2) may fly
         if (!(EOSV_ABL(a) & 1)) {
@@ -639,6 +640,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
         vm_wait<0>();
       }
       __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");  // no next-step DMA (an LDS write) moves above the barrier
     }
     return;
   }

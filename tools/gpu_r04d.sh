@@ -11,10 +11,10 @@ run() {  # name timeout cmd...
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "rc=$rc"; tail -n 4 "gpurun_out/$name.log" | cut -c1-600
-  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ] && { [ $rc -ne 1 ] || [ "$name" != pytest_gpu ]; }; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-[ -z "$SKIP_PYTEST" ] && run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread
+[ -z "$SKIP_PYTEST" ] && run pytest_gpu 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 600 python bench.py
 run trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o $TAG -- python bench.py --no-cpu-baseline

@@ -1,6 +1,6 @@
 """Repeat the backbone on identical inputs and report, per stage, how many runs differ bitwise
 from the first (an LDS / DMA ordering race shows up as run-to-run differences; every kernel is
-deterministic otherwise).  usage: python tools/race_probe.py [arch] [dtype] [reps]"""
+deterministic otherwise).  usage: python tools/race_probe.py [arch] [dtype] [reps] [frames]"""
 import os
 import sys
 
@@ -13,9 +13,10 @@ from eosv import arch, engine, synth  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
 dtype = sys.argv[2] if len(sys.argv) > 2 else "bf16"
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 12
+nf = int(sys.argv[4]) if len(sys.argv) > 4 else 37
 sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
-x = torch.randn(37, 3, 224, 224, generator=torch.Generator().manual_seed(5)).cuda()
-bb = engine.Backbone(name, dtype, 224, 224, max_frames=37)
+x = torch.randn(nf, 3, 224, 224, generator=torch.Generator().manual_seed(5)).cuda()
+bb = engine.Backbone(name, dtype, 224, 224, max_frames=nf)
 bb.load_state_dict(sd)
 for stage in range(5):
     ref = bb.probe(x, stage)
@@ -43,9 +44,9 @@ for stage in range(5):
               f"{nz[:, 1].unique().tolist()[:16]} channels {nz[:, 2].min().item()}..{nz[:, 2].max().item()} "
               f"({nz[:, 2].unique().numel()} distinct)", flush=True)
         # a 5-frame batch of the tail frames
-        t = bb.probe(x[32:37].contiguous(), stage)
-        print(f"   tail-only batch vs ref: {'equal' if torch.equal(t, ref[32:37]) else 'differs'}; "
-              f"vs first runs: {[torch.equal(t, o[32:37]) for o in outs[:4]]}", flush=True)
+        t = bb.probe(x[nf - 5:nf].contiguous(), stage)
+        print(f"   tail-only batch vs ref: {'equal' if torch.equal(t, ref[nf - 5:nf]) else 'differs'}; "
+              f"vs first runs: {[torch.equal(t, o[nf - 5:nf]) for o in outs[:4]]}", flush=True)
 ref = bb.forward(x)
 bad = sum(0 if torch.equal(bb.forward(x), ref) else 1 for _ in range(reps))
 print(f"{name} {dtype} forward: {bad}/{reps} runs differ", flush=True)
