@@ -339,12 +339,15 @@ static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::ve
   }
   // bf16 multi-tap convs with Cin > 64: K chunk-major, (cin / 64, kh, kw, cin % 64), so that a
   // conv's K walk visits all taps of one 64-channel slice of the input before the next slice.
-  // f32 multi-tap convs with Cin >= 128 (the implicit GEMM's; stage 1 takes the row kernel):
-  // (cin / 32, kh, kw, cin % 32), r04: in tap-major order a pixel's next tap came Cin / 16 K-steps
-  // later, when the XCD's 64 workgroups had staged ~8 MB and L2 (4 MB) had turned over, so the
-  // tap re-reads came from beyond L2 (PMC r03: 3.6x the algorithmic bytes); chunk-major brings
-  // them 2 K-steps later, and the two 64-B halves of a 128-B pixel line in consecutive K-steps
-  static const int f32kcm = env_switch("EOSV_F32_KCM", 32);  // f32 channel chunk; 0 = tap-major (A/B switch)
+  // f32 multi-tap convs with Cin >= 128 (the implicit GEMM's; stage 1 takes the row kernel) can
+  // take (cin / C, kh, kw, cin % C) too (EOSV_F32_KCM = C, profiling build): in tap-major order a
+  // pixel's next tap comes Cin / 16 K-steps later, when the XCD's 64 workgroups have staged ~8 MB
+  // and L2 (4 MB) has turned over, so the tap re-reads come from beyond L2.  r04 (PMC, R18 f32):
+  // C = 32 cuts the 256x128 tiles' FETCH_SIZE 3.0x and the fused-downsample ones' 5x, C = 64 2x,
+  // C = 128 1.1x, but the release kernels ran 2-4 % slower with C = 32 (profiling-build A/B:
+  // 0.3-0.5 %, C = 64 / 128 0.1-0.3 %): these convs are MFMA-bound with the DMA hidden, so
+  // tap-major stays the default
+  static const int f32kcm = env_switch("EOSV_F32_KCM", 0);  // f32 channel chunk (32, 64, 128); 0 = tap-major (A/B switch)
   c.kcmc = bf16 ? 64 : f32kcm;
   c.kcm = !c.stem && c.kcmc > 0 && c.cinp % c.kcmc == 0 && c.kh * c.kw > 1 && c.kwp == c.kw &&
           (bf16 ? c.cinp > 64 : c.cinp >= 128);
