@@ -317,6 +317,273 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
   }
 }
 
+// Warp-specialised tap-shift tile (r04, EOSV_BF16_TS_WS; bf16 layout): NW consumer waves (LDS
+// fragments + MFMAs only) and NP producer waves (LDS-DMA only), as conv_bf16_ws_kernel, on split
+// rings: 3 A slots (the stage's input row, two stages ahead) and 2 B slots (its 3 taps' weights,
+// one ahead), 147 KiB at 512 x 128.  Same stages, taps, MFMA order and epilogue as
+// conv_bf16_ts_kernel: bit-identical outputs.
+template <int BM, int BN, int WM, int WN, int NP>
+__global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(ConvArgs a) {
+  constexpr int BK = 32, NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int AR = (BM + 2 + 15) / 16 * 16, AP = AR / 16, APW = (AP + NP - 1) / NP;
+  constexpr int BP = 3 * BN / 16, BPW = (BP + NP - 1) / NP;
+  constexpr int AS = AR * BK, BS = 3 * BN * BK;  // bf16 elements per A / B slot
+  constexpr int SMEM = 3 * AS + 2 * BS;
+  __shared__ __attribute__((aligned(16))) u16 smem[SMEM];
+  auto a_slot = [&](int st) { return smem + (st % 3) * AS; };
+  auto b_slot = [&](int st) { return smem + 3 * AS + (st & 1) * BS; };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nN = a.Cout / BN;
+  const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
+  const int mt = bt / nN;
+  const int nt = bt - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const u16* zero = (const u16*)a.zero;
+  const int nst3 = 3 * (a.Cin / BK);
+  const int nst = nst3 + (a.x2 ? a.Cin2 / BK : 0);
+
+  if (wid >= NW) {  // ---------------------------------------------------------------- producer
+    const int pw = wid - NW;
+    const u16* __restrict__ x = (const u16*)a.x;
+    const u16* __restrict__ w = (const u16*)a.w;
+    const u16* x2 = (const u16*)a.x2;
+    const int lr = lane >> 2, sl = lane & 3;
+    const u16* apix[APW];
+    const u16* apix2[APW];
+    unsigned amask[APW];
+#pragma unroll
+    for (int t = 0; t < APW; ++t) {
+      const int piece = pw + NP * t;
+      const int row = piece * 16 + lr;
+      const int p = m0 - 1 + row;
+      apix[t] = zero;
+      apix2[t] = zero;
+      amask[t] = 0;
+      if (piece < AP && row <= BM + 1 && p >= 0 && p < M) {
+        const int img = p / HW, rem = p - img * HW;
+        const int oh = rem / a.W, ow = rem - oh * a.W;
+        apix[t] = x + (long long)p * a.xs + (sl ^ ((row >> 1) & 3)) * 8;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+          if ((unsigned)(oh + kh - 1) < (unsigned)a.H) amask[t] |= 1u << kh;
+        if (x2 && row >= 1 && row <= BM)
+          apix2[t] = x2 + (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.x2s +
+                     (sl ^ ((row >> 1) & 3)) * 8;
+      }
+    }
+    const u16* bsrc[BPW];
+    int btap[BPW];
+#pragma unroll
+    for (int t = 0; t < BPW; ++t) {
+      const int row = min((pw + NP * t) * 16, BP * 16 - 16) + lr;  // pieces past BP: never issued
+      const int kw = row / BN;
+      btap[t] = kw;
+      bsrc[t] = w + (long long)(n0 + row - kw * BN) * a.K + (sl ^ ((row >> 1) & 3)) * 8;
+    }
+    const long long rowoff = (long long)a.W * a.xs;
+    auto kidx = [&](int kh, int kw, int c) -> int {
+      return a.kcm ? (((c >> 6) * 9 + kh * 3 + kw) << 6) + (c & 63) : (kh * 3 + kw) * a.Cin + c;
+    };
+    auto stage_a = [&](int st) {
+      u16* As = a_slot(st);
+      if (st >= nst3) {  // DS stage: the x2 pixels (read at tap offset 1)
+        const int c0 = (st - nst3) * BK;
+#pragma unroll
+        for (int t = 0; t < APW; ++t)
+          if (pw + NP * t < AP) dma16(apix2[t] + (apix2[t] != zero ? c0 : 0), As + (pw + NP * t) * 16 * BK);
+        return;
+      }
+      const int cs = st / 3, kh = st - 3 * cs, c0 = cs * BK;
+      const long long aoff = (long long)(kh - 1) * rowoff + c0;
+#pragma unroll
+      for (int t = 0; t < APW; ++t)
+        if (pw + NP * t < AP) dma16(((amask[t] >> kh) & 1) ? apix[t] + aoff : zero, As + (pw + NP * t) * 16 * BK);
+    };
+    auto stage_b = [&](int st) {
+      u16* Bs = b_slot(st);
+      if (st >= nst3) {  // the 1x1 downsample's weights (K columns K1 + c) in tap slot 1
+        const int c0 = (st - nst3) * BK;
+#pragma unroll
+        for (int t = 0; t < BPW; ++t)
+          if (pw + NP * t < BP && btap[t] == 1) dma16(bsrc[t] + a.K1 + c0, Bs + (pw + NP * t) * 16 * BK);
+        return;
+      }
+      const int cs = st / 3, kh = st - 3 * cs, c0 = cs * BK;
+#pragma unroll
+      for (int t = 0; t < BPW; ++t)
+        if (pw + NP * t < BP) dma16(bsrc[t] + kidx(kh, btap[t], c0), Bs + (pw + NP * t) * 16 * BK);
+    };
+    // this wave's A pieces per stage (the last piece index goes to the first AP % NP waves)
+    const bool big = pw < AP - (APW - 1) * NP;
+    auto wait_a = [&]() {  // all but this wave's A pieces of the newest stage
+      if (big)
+        vm_wait<APW>();
+      else
+        vm_wait<APW - 1>();
+    };
+    if (nst > 0) {
+      stage_a(0);
+      stage_b(0);
+    }
+    if (nst > 1) {
+      stage_a(1);
+      wait_a();
+    } else {
+      vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int st = 0; st < nst; ++st) {  // B(st + 1), then A(st + 2); B(st + 1) and A(st + 1) land, A(st + 2) may fly
+      if (st + 1 < nst) stage_b(st + 1);
+      if (st + 2 < nst) {
+        stage_a(st + 2);
+        wait_a();
+      } else {
+        vm_wait<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------------------------ consumer
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r = lane & 15;
+  const int q = lane >> 4;
+  unsigned emask = 0;  // bit 2i: ow 0 (tap kw 0 reads padding), bit 2i + 1: ow W - 1 (kw 2)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / WM) + i * 16 + r;
+    const int ow = (m % HW) % a.W;
+    if (ow == 0) emask |= 1u << (2 * i);
+    if (ow == a.W - 1) emask |= 2u << (2 * i);
+  }
+  __builtin_amdgcn_s_barrier();  // stage 0 has landed
+  asm volatile("" ::: "memory");
+  for (int st = 0; st < nst; ++st) {
+    const u16* As = a_slot(st);
+    const u16* Bs = b_slot(st);
+    const bool ds = st >= nst3;  // a DS stage is read at offset 1 only (no taps, no edges)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      if (ds && kw != 1) continue;
+      bf16x8 bfr[TN], afr[2];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = kw * BN + wn * (BN / WN) + j * 16 + r;
+        bfr[j] = *(const bf16x8*)(Bs + row * BK + ((q ^ ((row >> 1) & 3)) * 8));
+      }
+      auto rdA = [&](int i) {
+        const int row = wm * (BM / WM) + i * 16 + r + kw;  // pixel m0 + (row - kw) at tap kw
+        bf16x8 f = *(const bf16x8*)(As + row * BK + ((q ^ ((row >> 1) & 3)) * 8));
+        if (kw != 1 && ((emask >> (2 * i + (kw >> 1))) & 1)) f = bf16x8{};
+        return f;
+      };
+      afr[0] = rdA(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (i + 1 < TM) afr[(i + 1) & 1] = rdA(i + 1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i + 1 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i & 1], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // epilogue (conv_bf16_ts_kernel's, consumer waves only, bf16 layout)
+  u16* __restrict__ y = (u16*)a.y;
+  const u16* __restrict__ res = (const u16*)a.res;
+  constexpr int EPR = WM * 32, EPS = BN + 4;
+  static_assert(EPR * EPS * 4 <= SMEM * 2, "epilogue tile must fit the ring");
+  float* ep = (float*)smem;
+  float bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bcol[j] = a.bias ? a.bias[n0 + wn * (BN / WN) + j * 16 + r] : 0.f;
+  constexpr int nthreads = 64 * NW;
+  constexpr int NPASS = BM / WM / 32;
+  constexpr int IPT = EPR * (BN / 8) / (64 * NW);
+  static_assert(IPT * 64 * NW == EPR * (BN / 8), "epilogue work divides evenly");
+  const long long ostr = a.Cout;
+  const long long tile_bytes = (long long)min(BM, M - m0) * ostr * 2;
+  const int nrec = (int)min(tile_bytes, 0x7fffffffLL);
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(y + (long long)m0 * ostr), (short)0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(res ? res + (long long)m0 * ostr : zero), (short)0, res ? nrec : 0, 0x00020000);
+  v4u rv[IPT];  // one residual set (two spilled at 168 VGPRs): pass i's load under its LDS write
+  auto chunk = [&](int i, int t, int& lrow, int& c8, int& voff) {
+    const int idx = tid + t * nthreads;
+    lrow = idx / (BN / 8);
+    c8 = idx - lrow * (BN / 8);
+    const int ml = (lrow >> 5) * (BM / WM) + i * 32 + (lrow & 31);
+    voff = (int)(((long long)ml * ostr + n0 + c8 * 8) * 2);
+  };
+  auto load_res = [&](int i) {
+#pragma unroll
+    for (int t = 0; t < IPT; ++t) {
+      int lrow, c8, voff;
+      chunk(i, t, lrow, c8, voff);
+      rv[t] = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, 0, 0);
+    }
+  };
+  const float rlow = a.relu ? 0.f : -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NPASS; ++i) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    load_res(i);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lrow = wm * 32 + t * 16 + 4 * q + e;
+          ep[lrow * EPS + wn * (BN / WN) + j * 16 + r] = acc[i * 2 + t][j][e] + bcol[j];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int t = 0; t < IPT; ++t) {
+      int lrow, c8, voff;
+      chunk(i, t, lrow, c8, voff);
+      const float4 v0 = *(const float4*)(ep + lrow * EPS + c8 * 8);
+      const float4 v1 = *(const float4*)(ep + lrow * EPS + c8 * 8 + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      const v4u r4 = rv[t];
+      const unsigned ru[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] += bf2f((u16)(ru[k] & 0xffff));
+        v[2 * k + 1] += bf2f((u16)(ru[k] >> 16));
+      }
+      v4u pk;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        pk[k] = (unsigned)f2bf(fmaxf(v[2 * k], rlow)) | ((unsigned)f2bf(fmaxf(v[2 * k + 1], rlow)) << 16);
+      __builtin_amdgcn_raw_buffer_store_b128(pk, yr, voff, 0, 0);
+    }
+  }
+}
+
 // shapes this kernel takes: stride-1 pad-1 3x3, Cin % 32, Cout 64 (512 x 64 tiles), 128 (512 x 128)
 // or a multiple of 256 (256 x 256), optionally a fused 1x1 downsample (Cin2 % 32), no stem
 bool conv_bf16_ts_ok(const ConvArgs& a) {
@@ -343,6 +610,17 @@ int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   else                                                                                                           \
     hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, false>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), \
                        0, s, a);
+  static const int tsws = env_switch("EOSV_BF16_TS_WS", 1);  // 1: warp-specialised 512 x 128 tile (A/B switch; r04: R18 layer-2 3x3s 7-10 %, R50 stage-2 3x3s 4-7 % faster)
+  if (tsws && !a.split && a.Cout == 128) {
+    constexpr int NT = 64 * (4 * 2 + 4);
+    if (a.plan) {
+      static const int occ = kernel_occupancy((const void*)conv_bf16_ts_ws_kernel<512, 128, 4, 2, 4>, NT);
+      return record_launch(a.plan, nb, occ);
+    }
+    hipLaunchKernelGGL((conv_bf16_ts_ws_kernel<512, 128, 4, 2, 4>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+    EOSV_LAUNCH_CHECK();
+    return EOSV_OK;
+  }
   if (a.Cout == 64) {
     TS_LAUNCH(512, 64, 8, 1)
   } else if (a.Cout == 128) {
