@@ -322,6 +322,236 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
   }
 }
 
+// Warp-specialised f32 tile (r04, EOSV_F32_WS): NW = WM x WN consumer waves that only read LDS
+// fragments and issue v_mfma_f32_32x32x2_f32, and NP producer waves that only stage A (im2col)
+// and B rows by LDS-DMA (each DMA piece costs its wave 60-185 cycles of issue, MI355X_MICROARCH.md;
+// in conv_f32_dma_kernel both waves of a SIMD issue theirs at the K-step's start).  Split rings:
+// 3 A slots (two K-steps ahead) and 2 B slots (one ahead); one barrier per K-step; producers
+// leave after the K loop.  Same K order, MFMA order and LDS-staged epilogue as conv_f32_dma_kernel
+// (EPI_LDS): bit-identical outputs.  Inference only (no split-K), tap-major or chunk-major K.
+// OCC: workgroups per CU the register budget is sized for (2 at NP 4: <= 80 VGPRs, 6 waves per SIMD;
+// 2 at NP 2: <= 96)
+template <int BM, int BN, int WM, int WN, int NP, bool DS, int OCC>
+__global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4) void conv_f32_ws_kernel(ConvArgs a) {
+  constexpr int BK = 16, CPR = BK / 4, RPI = 64 / CPR, RPB = 64 / BK;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int AI = BM / (RPI * NP), BI = BN / (RPI * NP);  // DMA pieces per producer wave
+  static_assert(AI >= 1 && BI >= 1 && AI * RPI * NP == BM && BI * RPI * NP == BN, "tile shape");
+  constexpr int AS = BM * BK, BS = BN * BK;  // floats per A / B slot
+  constexpr int EPS = BN + 4;
+  constexpr int SMEM = 3 * AS + 2 * BS > 32 * EPS ? 3 * AS + 2 * BS : 32 * EPS;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  auto a_slot = [&](int kt) { return smem + (kt % 3) * AS; };
+  auto b_slot = [&](int kt) { return smem + 3 * AS + (kt & 1) * BS; };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int HoWo = a.Ho * a.Wo;
+  const int M = a.N * HoWo;
+  const int nN = (a.Cout + BN - 1) / BN;
+  const int bt = xcd_tile(blockIdx.x, gridDim.x, a.xcd);
+  const int mt = bt / nN;
+  const int nt = bt - mt * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nk = a.K / BK;
+
+  if (wid >= NW) {  // ---------------------------------------------------------------- producer
+    const int pw = wid - NW;
+    const float* __restrict__ x = (const float*)a.x;
+    const float* __restrict__ w = (const float*)a.w;
+    const float* zero = (const float*)a.zero;
+    const int lr = lane / CPR, pc = lane % CPR;
+    const float* arow[AI];
+    const float* arow2[DS ? AI : 1];
+    int aih[AI], aiw[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int row = pw * (BM / NP) + RPI * j + lr;
+      const int lc = pc ^ ((row / RPB) & (CPR - 1));
+      const int m = m0 + row;
+      if (m < M) {
+        const int img = m / HoWo, rem = m - img * HoWo, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        aih[j] = oh * a.stride - a.pad;
+        aiw[j] = ow * a.stride - a.pad;
+        arow[j] = x + (((long long)img * a.H + aih[j]) * a.W + aiw[j]) * a.Cin + lc * 4;
+        if constexpr (DS)
+          arow2[j] = (const float*)a.x2 + (((long long)img * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 + lc * 4;
+      } else {
+        aih[j] = -(1 << 28);
+        aiw[j] = 0;
+        arow[j] = x;
+        if constexpr (DS) arow2[j] = nullptr;
+      }
+    }
+    const float* brow[BI];
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int row = pw * (BN / NP) + RPI * j + lr;
+      const int lc = pc ^ ((row / RPB) & (CPR - 1));
+      const int n = n0 + row;
+      brow[j] = n < a.Cout ? w + (long long)n * a.K + lc * 4 : nullptr;
+    }
+    // tap counters of the next A stage (A stages are issued in K order)
+    const int KC = a.kcm;
+    int nc0 = 0, nkw = 0, nkh = 0;
+    auto stage_a = [&](int kt) {
+      float* As = a_slot(kt);
+      const int k0 = kt * BK;
+      if (DS && k0 >= a.K1) {
+#pragma unroll
+        for (int j = 0; j < (DS ? AI : 1); ++j) {
+          const float* src = arow2[j] ? arow2[j] + (k0 - a.K1) : zero;
+          __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(As + (pw * (BM / NP) + RPI * j) * BK), 16, 0, 0);
+        }
+        return;
+      }
+      const int kh = nkh, kw = nkw;
+      const long long toff = ((long long)kh * a.W + kw) * a.Cin + nc0;
+      nc0 += BK;
+      if (KC) {
+        if ((nc0 & (KC - 1)) == 0) {
+          nc0 -= KC;
+          if (++nkw == a.KW) {
+            nkw = 0;
+            if (++nkh == a.KH) nkh = 0, nc0 += KC;
+          }
+        }
+      } else if (nc0 == a.Cin) {
+        nc0 = 0;
+        if (++nkw == a.KW) nkw = 0, ++nkh;
+      }
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const int ih = aih[j] + kh, iw = aiw[j] + kw;
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const float* src = ok ? arow[j] + toff : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(As + (pw * (BM / NP) + RPI * j) * BK), 16, 0, 0);
+      }
+    };
+    auto stage_b = [&](int kt) {
+      float* Bs = b_slot(kt);
+#pragma unroll
+      for (int j = 0; j < BI; ++j) {
+        const float* src = brow[j] ? brow[j] + kt * BK : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(Bs + (pw * (BN / NP) + RPI * j) * BK), 16, 0, 0);
+      }
+    };
+    if (nk > 0) {
+      stage_a(0);
+      stage_b(0);
+    }
+    if (nk > 1) {
+      stage_a(1);
+      vm_wait<AI>();
+    } else {
+      vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int kt = 0; kt < nk; ++kt) {  // B(kt + 1), then A(kt + 2); B(kt + 1) and A(kt + 1) land
+      if (kt + 1 < nk) stage_b(kt + 1);
+      if (kt + 2 < nk) {
+        stage_a(kt + 2);
+        vm_wait<AI>();
+      } else {
+        vm_wait<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------------------------ consumer
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int h = lane >> 5;
+  const int r = lane & 31;
+  const int sw = (r / RPB) & (CPR - 1);
+  __builtin_amdgcn_s_barrier();  // stage 0 has landed
+  asm volatile("" ::: "memory");
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* As = a_slot(kt);
+    const float* Bs = b_slot(kt);
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const int pch = ((h * (BK / 8) + g) ^ sw) * 4;
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *(const f32x4*)(As + (wm * (BM / WM) + i * 32 + r) * BK + pch);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *(const f32x4*)(Bs + (wn * (BN / WN) + j * 32 + r) * BK + pch);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s4], bf[j][s4], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // epilogue (conv_f32_dma_kernel's EPI_LDS one; consumer waves only)
+  float* __restrict__ y = (float*)a.y;
+  const float* __restrict__ res = (const float*)a.res;
+  float bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + r;
+    bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+  }
+  float* ep = smem;
+  constexpr int nthreads = 64 * NW;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    for (int wsel = 0; wsel < WM; ++wsel) {
+      __syncthreads();
+      if (wm == wsel) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            ep[((q & 3) + 8 * (q >> 2) + 4 * h) * EPS + wn * (BN / WN) + j * 32 + r] = acc[i][j][q] + bcol[j];
+      }
+      __syncthreads();
+      for (int idx = tid; idx < 32 * (BN / 4); idx += nthreads) {
+        const int lrow = idx / (BN / 4);
+        const int c4 = idx - lrow * (BN / 4);
+        const int m = m0 + wsel * (BM / WM) + i * 32 + lrow;
+        const int n = n0 + c4 * 4;
+        if (m >= M || n >= a.Cout) continue;
+        float4 v = *(const float4*)(ep + lrow * EPS + c4 * 4);
+        const long long o = (long long)m * a.Cout + n;
+        if (res) {
+          const float4 rv = *(const float4*)(res + o);
+          v.x += rv.x;
+          v.y += rv.y;
+          v.z += rv.z;
+          v.w += rv.w;
+        }
+        if (a.relu) {
+          v.x = fmaxf(v.x, 0.f);
+          v.y = fmaxf(v.y, 0.f);
+          v.z = fmaxf(v.z, 0.f);
+          v.w = fmaxf(v.w, 0.f);
+        }
+        *(float4*)(y + o) = v;
+      }
+    }
+  }
+}
+
 // split-K (training entry only): enough slices to put ~2 workgroups on every CU, each slice at
 // least 32 K-steps, at most 8
 static int ksplit_count(long long blocks, int ksteps) {
@@ -389,6 +619,34 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
   return EOSV_OK;
 }
 
+// EOSV_F32_WS (r04): the warp-specialised tiles for the Cout >= 128 implicit-GEMM convs of the
+// inference path (no split-K workspace): 1 one workgroup per CU (90 VGPRs), 2 two (80 VGPRs), 3 two
+// workgroups of 2 producer waves each (96 VGPRs).
+static int f32_ws() {
+  static const int v = env_switch("EOSV_F32_WS", 0);  // (A/B switch)
+  return v;
+}
+
+template <int BM, int BN, int WM, int WN, int OCC, int NP = 4>
+static int launch_ws(const ConvArgs& a, hipStream_t s) {
+  constexpr int NT = 64 * (WM * WN + NP);
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  const long long nb = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  if (nb > 0x7fffffffLL) return set_error("conv: grid too large"), EOSV_ERR_UNSUPPORTED;
+  if (a.plan) {
+    static const int occ = kernel_occupancy((const void*)conv_f32_ws_kernel<BM, BN, WM, WN, NP, false, OCC>, NT);
+    return record_launch(a.plan, nb, occ);
+  }
+  if (a.x2) {
+    if (a.K1 % 16 || a.Cin2 % 16) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL((conv_f32_ws_kernel<BM, BN, WM, WN, NP, true, OCC>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_f32_ws_kernel<BM, BN, WM, WN, NP, false, OCC>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+  }
+  EOSV_LAUNCH_CHECK();
+  return EOSV_OK;
+}
+
 // Cout > 64 tiles: small batches (the training step: 96 frames) give grids below the chip's CU
 // count, so the tile shrinks (same BK, same k-order per output: bit-identical results).
 // 1 = 256x128, 2 = 128x128, 3 = 128x64.
@@ -435,6 +693,17 @@ int launch_conv_f32(const ConvArgs& a0, hipStream_t s) {
   if (tile == 5) return launch_dma<512, 128, 16, 4, 2, false>(a, s);  // 8 waves of 128x64
   if (tile == 6 && a.Cout <= 256) return launch_dma<512, 128, 16, 4, 2, false>(a, s);
 #endif
+  if (f32_ws() && !a.kws) {
+    const int t = f32_tile(a);
+    if (t == 1) {
+      if (f32_ws() == 3) return launch_ws<256, 128, 4, 2, 2, 2>(a, s);
+      return f32_ws() == 2 ? launch_ws<256, 128, 4, 2, 2>(a, s) : launch_ws<256, 128, 4, 2, 1>(a, s);
+    }
+    if (t == 2) {
+      if (f32_ws() == 3) return launch_ws<128, 128, 2, 2, 2, 2>(a, s);
+      return f32_ws() == 2 ? launch_ws<128, 128, 2, 2, 2>(a, s) : launch_ws<128, 128, 2, 2, 1>(a, s);
+    }
+  }
   switch (f32_tile(a)) {
     case 1: return launch_dma<256, 128, 16, 4, 2, false>(a, s);
     case 2: return launch_dma<128, 128, 16, 2, 2, false>(a, s);
