@@ -810,8 +810,11 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
 // EOSV_BF16_WS bits (bf16 layout only): 1 stride-1 multi-tap convs on 256x256 tiles (split
 // rings), 2 the other 256x256 convs (1x1, stride 2, folded downsample; split rings), 4 the 512x128
 // tiles (one ring).
+#ifndef EOSV_BF16_WS_DEF
+#define EOSV_BF16_WS_DEF 7
+#endif
 static int bf16_ws() {
-  static const int v = env_switch("EOSV_BF16_WS", 7);  // (A/B switch)
+  static const int v = env_switch("EOSV_BF16_WS", EOSV_BF16_WS_DEF);  // (A/B switch)
   return v;
 }
 

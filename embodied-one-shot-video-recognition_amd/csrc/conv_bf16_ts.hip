@@ -592,6 +592,10 @@ bool conv_bf16_ts_ok(const ConvArgs& a) {
          a.Wo == a.W && a.Cin % 32 == 0 && ds_ok && (a.Cout == 64 || a.Cout == 128 || a.Cout % 256 == 0) && a.zero;
 }
 
+#ifndef EOSV_BF16_TS_WS_DEF
+#define EOSV_BF16_TS_WS_DEF 1
+#endif
+
 int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   if (!conv_bf16_ts_ok(a)) return set_error("conv_bf16_ts: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   const long long M = (long long)a.N * a.Ho * a.Wo;
@@ -610,7 +614,7 @@ int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   else                                                                                                           \
     hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, false>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), \
                        0, s, a);
-  static const int tsws = env_switch("EOSV_BF16_TS_WS", 1);  // 1: warp-specialised 512 x 128 tile (A/B switch; r04: R18 layer-2 3x3s 7-10 %, R50 stage-2 3x3s 4-7 % faster)
+  static const int tsws = env_switch("EOSV_BF16_TS_WS", EOSV_BF16_TS_WS_DEF);  // 1: warp-specialised 512 x 128 tile (A/B switch; r04: R18 layer-2 3x3s 7-10 %, R50 stage-2 3x3s 4-7 % faster)
   if (tsws && !a.split && a.Cout == 128) {
     constexpr int NT = 64 * (4 * 2 + 4);
     if (a.plan) {

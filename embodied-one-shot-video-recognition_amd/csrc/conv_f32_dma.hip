@@ -622,8 +622,11 @@ static int launch_dma(const ConvArgs& a, hipStream_t s) {
 // EOSV_F32_WS (r04): the warp-specialised tiles for the Cout >= 128 implicit-GEMM convs of the
 // inference path (no split-K workspace): 1 one workgroup per CU (90 VGPRs), 2 two (80 VGPRs), 3 two
 // workgroups of 2 producer waves each (96 VGPRs).
+#ifndef EOSV_F32_WS_DEF
+#define EOSV_F32_WS_DEF 2
+#endif
 static int f32_ws() {
-  static const int v = env_switch("EOSV_F32_WS", 2);  // (A/B switch; r04: 2 is 4 % faster than 0 on R18 f32, 3 is 5 % slower than 0)
+  static const int v = env_switch("EOSV_F32_WS", EOSV_F32_WS_DEF);  // (A/B switch; r04: 2 is 4 % faster than 0 on R18 f32, 3 is 5 % slower than 0)
   return v;
 }
 
