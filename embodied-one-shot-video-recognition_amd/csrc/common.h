@@ -178,6 +178,8 @@ struct Pair1x1Args {
 };
 bool pair1x1_bf16_ok(int cmid, int cexp, int c1, int cds, long long M);
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
+// pair1x1r_bf16.hip (r04): the same pair with each wave owning its pixels for both GEMMs
+int launch_pair1x1r_bf16(const Pair1x1Args& a, hipStream_t s);
 // pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
 // streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
 int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128 or 256)
