@@ -282,11 +282,17 @@ static int launch_pair(const Pair1x1Args& a, long long ntiles, hipStream_t s) {
   return EOSV_OK;
 }
 
+#ifndef EOSV_PAIR_R_DEF
+#define EOSV_PAIR_R_DEF 1
+#endif
+
 int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s) {
   if (!pair1x1_bf16_ok(64, 256, a.c1, a.cds, a.M) || !a.x || !a.w3 || !a.b3 || !a.w1 || !a.b1 || !a.y || !a.z ||
       (a.cds ? !a.x2 : !a.res))
     return set_error("pair1x1_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
-  static const int pr = env_switch("EOSV_PAIR_R", 0);  // 1: pair1x1r_bf16 (pixels per wave, A/B switch)
+  // 1: pair1x1r_bf16 (pixels per wave; A/B switch; r04: R50 layer1.0 pair 1.96 -> 1.64 ms, layer1.2
+  // pair 2.83 -> 2.50, layer1.1 pair 2.34 -> 2.33, bit-identical)
+  static const int pr = env_switch("EOSV_PAIR_R", EOSV_PAIR_R_DEF);
   if (pr) return launch_pair1x1r_bf16(a, s);
   const long long ntiles = a.M / PAIR_BM;
   if (a.cds) return launch_pair<64, true>(a, ntiles, s);
