@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64 * PR_NW) void pair1x1r_bf16_kernel(Pair1x1Args a
   constexpr int NCH = 4;              // 64-channel chunks of Y (256)
   constexpr int PX = 16 * NPT;        // pixels per wave per round
   constexpr int TILE = PX * PR_NW;    // pixels per round
-  constexpr int RD = 1;               // residual chunks loaded ahead (a chunk is ~3.5 us of a CU's HBM time at 256-pixel rounds)
+  constexpr int RD = NPT == 1 && C1 == 64 ? 2 : 1;  // residual chunks loaded ahead (2 spilled 5-6 VGPRs at NPT 2 or C1 128)
   constexpr int NRS = 4;              // residual register sets: a ring of NCH, so a chunk's set is the same in every round
   __shared__ __attribute__((aligned(16))) u16 smem[256 * K3 + C1 * 256 + 2 * (256 + C1)];
   u16* const W3s = smem;
@@ -260,7 +260,8 @@ int launch_pair1x1r_bf16(const Pair1x1Args& a, hipStream_t s) {
       !a.b3 || !a.w1 || !a.b1 || !a.y || !a.z || (a.cds ? !a.x2 : !a.res))
     return set_error("pair1x1r_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   if (a.cds) return launch_pr<64, true, 2>(a, s);
-  if (a.c1 == 64) return launch_pr<64, false, 2>(a, s);
+  static const int npt1 = env_switch("EOSV_PAIR_R_NPT1", 0);  // 1: the residual c1-64 pair on 128-pixel rounds (A/B switch)
+  if (a.c1 == 64) return npt1 ? launch_pr<64, false, 1>(a, s) : launch_pr<64, false, 2>(a, s);
   return launch_pr<128, false, 1>(a, s);
 }
 
