@@ -423,6 +423,36 @@ static void add_plan_cost(eosv_handle* h, const LaunchInfo& li, double flops) {
   h->plan_cost += flops * rounds * (double)li.slots / (double)li.blocks;
 }
 
+#ifdef EOSV_PROFILING
+// Poisoning (profiling build, EOSV_POISON bits, read per call): 1 fills the activation buffers with
+// 0xff bytes (NaN in bf16 and f32) at every chunk's start, 2 fills every CU's LDS with 0xff before
+// every launch, 4 synchronises the stream before (and after) that.  A kernel whose valid outputs depend on an activation row or an LDS word that it
+// (or the layer before) did not write then yields NaN or different features, in the first run:
+// tools/poison_check.py compares poisoned and plain forwards bit for bit.
+__global__ __launch_bounds__(256) void lds_poison_kernel() {
+  __shared__ unsigned lds[160 * 1024 / 4];
+  volatile unsigned* p = lds;
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 256) p[i] = 0xffffffffu;
+}
+static int poison_mode() { return env_switch("EOSV_POISON", 0); }
+static void poison_lds(hipStream_t s) {
+  if (poison_mode() & 4) (void)hipStreamSynchronize(s);  // 4: the previous launch has drained
+  if (poison_mode() & 2) hipLaunchKernelGGL(lds_poison_kernel, dim3(4 * device_cu_count()), dim3(256), 0, s);
+  if (poison_mode() & 4) (void)hipStreamSynchronize(s);
+}
+static int poison_bufs(eosv_handle* h, hipStream_t s) {
+  if (!(poison_mode() & 1)) return EOSV_OK;
+  const size_t elt = act_bytes(h);
+  for (void* p : h->buf) EOSV_HIP_CHECK(hipMemsetAsync(p, 0xff, (size_t)h->d.max_frames * h->act_elems * elt, s));
+  for (void* p : h->sbuf)
+    if (p) EOSV_HIP_CHECK(hipMemsetAsync(p, 0xff, (size_t)h->sub_frames * h->act_elems * elt, s));
+  return EOSV_OK;
+}
+#else
+static void poison_lds(hipStream_t) {}
+static int poison_bufs(eosv_handle*, hipStream_t) { return EOSV_OK; }
+#endif
+
 static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, int W, const void* res,
                     void* y, bool relu, bool bf16, hipStream_t s, const void* x2 = nullptr, int H2 = 0,
                     int W2 = 0, int stride2 = 1) {
@@ -471,6 +501,7 @@ static int run_conv(eosv_handle* h, const Conv& c, const void* x, int N, int H, 
     if (prc == EOSV_OK) add_plan_cost(h, li, flops);
     return prc;
   }
+  poison_lds(s);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);
@@ -553,6 +584,7 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
     if (prc == EOSV_OK) add_plan_cost(h, li, flops);
     return prc;
   }
+  poison_lds(s);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (h->prof) {
     e0 = prof_event(h);
@@ -647,6 +679,7 @@ static int run_stem(eosv_handle* h, const float* frames, int B, void* const* buf
   const bool x3stem = x3(h) && direct && x3_split_stem && h->stem_x3.w && stem_pool_x3_ok(H, W);
   const bool fused = stem_pool_fused(sbf) && (sbf ? stem_pool_bf16_ok(H, W, direct) : stem_pool_f32_ok(H, W));
   if (x3(h) && !fused && !x3stem) return set_error("f32x3: needs the fused stem + maxpool (frame width)"), EOSV_ERR_UNSUPPORTED;
+  if (!h->planning) poison_lds(s);
   // the bf16 and f32 fused stems read the f32 NCHW frames themselves (no pack pass)
   const bool direct_bf = fused && sbf && direct;
   const bool direct_f32 = fused && !sbf && direct && stem_pool_f32_direct_ok(H, W);
@@ -705,6 +738,7 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
   int rc;
   void* x;
   int hh = h->hp, ww = h->wp;
+  if (!h->planning && (rc = poison_bufs(h, s))) return rc;
   if (h->sub_frames > 0 && h->sub_frames < B) {
     // Front stages (stem, maxpool, layer1: the largest activations) run on sub-chunks whose
     // working set stays in the 256 MiB Infinity Cache; each sub-chunk's layer1 output lands
@@ -725,6 +759,7 @@ static int forward_chunk(eosv_handle* h, const float* frames, int B, float* feat
     if ((rc = run_blocks(h, 0, h->blocks.size(), h->buf[1], h->buf, B, hh, ww, nullptr, &x, bf, s))) return rc;
   }
   if (h->planning) return EOSV_OK;
+  poison_lds(s);
   return launch_avgpool(x, B, hh * ww, h->D, feat, x3(h) ? 2 : bf ? 1 : 0, s);
 }
 
@@ -920,6 +955,7 @@ int eosv_backbone_probe(eosv_handle* h, const float* d_frames, int B, int stage,
   const bool bf = conv_bf(h);
   const hipStream_t s = (hipStream_t)stream;
   int rc;
+  if ((rc = poison_bufs(h, s))) return rc;
   if ((rc = run_stem(h, d_frames, B, h->buf, bf, s))) return rc;
   void* x = h->buf[1];
   int hh = h->hp, ww = h->wp;

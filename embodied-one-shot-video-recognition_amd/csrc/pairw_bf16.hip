@@ -440,12 +440,16 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   return EOSV_OK;
 }
 
-// 16-pixel tiles per wave of the pair for this shape (EOSV_PAIRW_NPT2=0 in the profiling build:
-// NPT 1 everywhere, the r03 form)
+// 16-pixel tiles per wave of the pair for this shape: NPT 1 everywhere (the r03 form).  NPT 2 (the
+// stage-2 pair with C1 = 128 on 256-pixel rounds, r04: 1.45 -> 1.34 ms per launch) is off in both
+// builds: in the backbone it gave run-to-run different R50 / R101 features at 64 and 130 frames
+// per chunk (tools/race_modes.py: 4 of 4 plain repeats distinct; 0 with NPT 1), while the same
+// kernel alone, in place and under cold caches and poisoned LDS, stayed bitwise equal to the
+// unfused convs (tests/native/conv_check pairw_stress).  EOSV_PAIRW_NPT2=1 (profiling build)
+// brings it back for study.  NPT 2 fits the register file only without the downsample's 8 extra
+// X fragments (the block-0 pair spills 55 VGPRs at NPT 2) and at C1 = 128.
 static int pairw_npt(int cmid, int c1, int cds) {
-  // NPT 2 fits the register file only without the downsample's 8 extra X fragments (the block-0
-  // pair spills 55 VGPRs at NPT 2) and at C1 = 128 (C1 = 256: 128 accumulator VGPRs more)
-  static const int npt2 = env_switch("EOSV_PAIRW_NPT2", 1);
+  static const int npt2 = env_switch("EOSV_PAIRW_NPT2", 0);
   return npt2 && cmid == 128 && c1 == 128 && cds == 0 ? 2 : 1;
 }
 

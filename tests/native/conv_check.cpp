@@ -518,7 +518,17 @@ static int check_pair(int N, int H, int W, int c1, bool ds) {
 // need not be a multiple of the 128-pixel round: the tail round runs on the buffers' padding
 // (filled with NaN here: no valid output may depend on it), and it is repeated REPS times (its
 // results changed from run to run while it masked the padding with out-of-range buffer ops).
-static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds = 0) {
+// every CU's LDS filled with 0xff (NaN in bf16): a kernel reading LDS words it did not write
+__global__ __launch_bounds__(256) void lds_poison_k() {
+  __shared__ unsigned lds[160 * 1024 / 4];
+  volatile unsigned* q = lds;
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 256) q[i] = 0xffffffffu;
+}
+
+// inplace: y = res (as the engine runs the pair: Y lands in the residual's buffer); stress: before
+// every repetition 1 GiB is written (cold caches) and the LDS poisoned
+static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds = 0, bool inplace = false,
+                       bool stress = false, int reps = 0) {
   // cds > 0: block 0 of a stage, conv3 + the folded stride-2 downsample reading x2 [N][2H][2W][cds]
   // (ragged: 2H - 1 when odd sizes are asked for through H2/W2 below), no residual
   const long long M = (long long)N * H * W;
@@ -571,9 +581,17 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   long bady = 0, badz = 0;
   double maxd = 0;
   int rcp = 0;
-  const int REPS = M % tile ? 8 : 1;
+  const int REPS = reps ? reps : M % tile ? 8 : 1;
+  void* flush = nullptr;
+  if (stress) hipMalloc(&flush, 1LL << 30);
+  if (inplace && !cds) p.res = y1;
   for (int rep = 0; rep < REPS; ++rep) {
     hipMemset(y1, 0xff, Mp * cexp * 2); hipMemset(z1, 0xff, Mp * c1 * 2);
+    if (inplace && !cds) hipMemcpy(y1, dr, M * cexp * 2, hipMemcpyDeviceToDevice);
+    if (stress) {
+      hipMemset(flush, rep, 1LL << 30);
+      hipLaunchKernelGGL(lds_poison_k, dim3(1024), dim3(256), 0, 0);
+    }
     rcp |= launch_pairw_bf16(p, 0);
     hipDeviceSynchronize();
     hipMemcpy(hy1.data(), y1, M * cexp * 2, hipMemcpyDeviceToHost);
@@ -601,12 +619,20 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   const bool fail = rc || rcp || bady || badz || maxerr > 1e-2;
   printf("%s pairw bf16 N%d H%d W%d %d(+ds %d)->%d->%d M%lld rc=%d/%d differing y %ld z %ld (max %.3e) unfused maxerr %.3e\n",
          fail ? "FAIL" : "ok  ", N, H, W, cmid, cds, cexp, c1, M, rc, rcp, bady, badz, maxd, maxerr);
-  for (void* q : {dx, dr, dx2, dw3, dw1, (void*)db3, (void*)db1, y0, y1, z0, z1, dz}) hipFree(q);
+  for (void* q : {dx, dr, dx2, dw3, dw1, (void*)db3, (void*)db1, y0, y1, z0, z1, dz, flush}) hipFree(q);
   return fail ? 1 : 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int fails = 0;
+  if (argc > 1 && !strcmp(argv[1], "pairw_stress")) {  // the engine's in-place pairs at C2/C3 chunk sizes
+    for (int n : {64, 130, 43, 257})
+      for (int c1 : {128, 256}) fails += check_pairw(n, 28, 28, 128, 512, c1, 0, true, true, 4);
+    fails += check_pairw(64, 14, 14, 256, 1024, 256, 0, true, true, 4);
+    fails += check_pairw(64, 28, 28, 128, 512, 128, 256, false, true, 4);
+    printf("%d failures\n", fails);
+    return fails ? 1 : 0;
+  }
   // R50 layer2 / layer3 wide pairs: within a stage (c1 = cmid) and into the next stage; many rounds
   // per workgroup (300 x 784 = 1838 rounds), ragged M (3 x 196 = 588: 4.6 rounds), tiny M
   fails += check_pairw(300, 28, 28, 128, 512, 128);

@@ -253,6 +253,25 @@ def test_backbone_repeat_determinism(dtype, name):
         bb.close()
 
 
+@pytest.mark.parametrize("name", ["resnet50", "resnet101"])
+def test_backbone_determinism_over_chunk_sizes(name):
+    """bf16 features bitwise equal over repeated forwards at chunk sizes whose persistent-kernel
+    grids end differently (one round per workgroup, 1-2 rounds, several).  r04's stage-2 pair on
+    256-pixel rounds gave different features in every repeat at 64 and 130 frames and none at 37,
+    257 or 1024 (tools/race_modes.py): the 37-frame test above missed it."""
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    bb = engine.Backbone(name, "bf16", 224, 224, max_frames=130)
+    bb.load_state_dict(sd)
+    try:
+        for nf in (64, 130, 17):
+            x = torch.randn(nf, 3, 224, 224, generator=torch.Generator().manual_seed(nf)).cuda()
+            ref = bb.forward(x)
+            for _ in range(4):
+                assert torch.equal(bb.forward(x), ref), f"{name} {nf} frames: features changed between identical runs"
+    finally:
+        bb.close()
+
+
 def test_full_size_c2_f32_bf16_agreement():
     """Config 2 at its full shape (224², T=16, R18, 400 episodes = 38,400 frames through
     the chunked forward): f32 and bf16 predict the same class on >= 97 % of the episodes,

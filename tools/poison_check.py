@@ -1,0 +1,69 @@
+"""Poisoned vs plain forwards (profiling build, EOSV_POISON): every activation buffer filled with
+0xff bytes (NaN in bf16 / f32) at each chunk's start and every CU's LDS filled with 0xff before
+each launch.  A kernel whose valid outputs read activation rows or LDS words nobody wrote then
+gives NaN or different features on the FIRST run, independent of timing, so one pass over the
+batch sizes below is the check (no repetition).  Per case: stage maps 0-4 and features, bitwise.
+
+  EOSV_LIBRARY=.../libeosv_prof.so python tools/poison_check.py [arch,...] [dtype,...] [frames,...]
+"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "embodied-one-shot-video-recognition_amd"))
+from eosv import arch, engine, synth  # noqa: E402
+
+archs = (sys.argv[1] if len(sys.argv) > 1 else "resnet50,resnet18,resnet101").split(",")
+dtypes = (sys.argv[2] if len(sys.argv) > 2 else "bf16,f32,f32x3").split(",")
+counts = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "1,3,17,64,130,257").split(",")]
+
+
+def run(bb, x, mode):
+    os.environ["EOSV_POISON"] = str(mode)
+    outs = [bb.probe(x, st) for st in range(5)] + [bb.forward(x)]
+    torch.cuda.synchronize()
+    os.environ["EOSV_POISON"] = "0"
+    return outs
+
+
+MODE = int(os.environ.get("POISON_MODE", "3"))  # EOSV_POISON bits of the poisoned run
+fails = 0
+for name in archs:
+    sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
+    for dtype in dtypes:
+        nmax = max(counts)
+        bb = engine.Backbone(name, dtype, 224, 224, max_frames=nmax)
+        bb.load_state_dict(sd)
+        for nf in counts:
+            x = torch.randn(nf, 3, 224, 224, generator=torch.Generator().manual_seed(nf)).cuda()
+            plain = run(bb, x, 0)
+            pois = run(bb, x, MODE)
+            bad = []
+            for i, (a, b) in enumerate(zip(plain, pois)):
+                if not torch.equal(a, b):
+                    d = (a - b).abs().flatten(1)
+                    fr = torch.nonzero(torch.isnan(d).any(1) | (d.nan_to_num(1.0).amax(1) > 0)).flatten().tolist()
+                    bad.append(f"{'stage %d' % i if i < 5 else 'features'}: frames {fr[:8]}{'...' if len(fr) > 8 else ''}"
+                               f" nan {int(torch.isnan(b).sum())}")
+            print(f"{name} {dtype} frames {nf}: {'OK' if not bad else 'DIFFERS ' + '; '.join(bad)}", flush=True)
+            fails += bool(bad)
+        # multi-chunk: the same frames through a handle that holds fewer than them
+        if nmax > 8:
+            bb.close()
+            bb = engine.Backbone(name, dtype, 224, 224, max_frames=nmax // 3)
+            bb.load_state_dict(sd)
+            x = torch.randn(nmax, 3, 224, 224, generator=torch.Generator().manual_seed(99)).cuda()
+            os.environ["EOSV_POISON"] = "0"
+            a = bb.forward(x)
+            os.environ["EOSV_POISON"] = str(MODE)
+            b = bb.forward(x)
+            torch.cuda.synchronize()
+            os.environ["EOSV_POISON"] = "0"
+            ok = torch.equal(a, b)
+            print(f"{name} {dtype} frames {nmax} in chunks of <= {nmax // 3}: {'OK' if ok else 'DIFFERS'}", flush=True)
+            fails += not ok
+        bb.close()
+print(f"poison_check: {fails} failing case(s)")
+sys.exit(1 if fails else 0)
