@@ -9,6 +9,7 @@
 #include <hip/hip_bf16.h>
 
 #include <cmath>
+#include <cstdio>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -592,11 +593,50 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
     if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
     EOSV_HIP_CHECK(hipEventRecord(e0, s));
   }
+#ifdef EOSV_PROFILING
+  // EOSV_POISON bit 8: every pair runs a second time out of place (residual copied first) into
+  // scratch, and both outputs are compared bytewise on the host (stderr): does the pair's own
+  // output change between two runs on the same inputs inside the backbone?
+  static void* scr[3] = {nullptr, nullptr, nullptr};
+  const bool selfcheck = (poison_mode() & 8) != 0;
+  const size_t cap_b = (size_t)p.cap_elems * 2;
+  if (selfcheck) {
+    for (auto& q : scr)
+      if (!q) EOSV_HIP_CHECK(hipMalloc(&q, cap_b));
+    if (res) EOSV_HIP_CHECK(hipMemcpyAsync(scr[0], res, cap_b, hipMemcpyDeviceToDevice, s));
+  }
+#endif
   const int rc = wide ? launch_pairw_bf16(p, s) : launch_pair1x1_bf16(p, s);
   if (h->prof && rc == EOSV_OK) {
     EOSV_HIP_CHECK(hipEventRecord(e1, s));
     h->recs.push_back({b.c3.id, e0, e1, flops});
   }
+#ifdef EOSV_PROFILING
+  if (selfcheck && rc == EOSV_OK) {
+    Pair1x1Args q = p;
+    if (res) q.res = scr[0];
+    q.y = scr[1];
+    q.z = scr[2];
+    const int rc2 = wide ? launch_pairw_bf16(q, s) : launch_pair1x1_bf16(q, s);
+    EOSV_HIP_CHECK(hipStreamSynchronize(s));
+    const size_t ny = (size_t)M * p.cexp, nz = (size_t)M * p.c1;
+    std::vector<unsigned short> a(ny), c(ny);
+    long long dy = 0, dz = 0, fy = -1, fz = -1;
+    EOSV_HIP_CHECK(hipMemcpy(a.data(), y, ny * 2, hipMemcpyDeviceToHost));
+    EOSV_HIP_CHECK(hipMemcpy(c.data(), scr[1], ny * 2, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ny; ++i)
+      if (a[i] != c[i] && dy++ == 0) fy = (long long)i;
+    a.resize(nz);
+    c.resize(nz);
+    EOSV_HIP_CHECK(hipMemcpy(a.data(), z, nz * 2, hipMemcpyDeviceToHost));
+    EOSV_HIP_CHECK(hipMemcpy(c.data(), scr[2], nz * 2, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nz; ++i)
+      if (a[i] != c[i] && dz++ == 0) fz = (long long)i;
+    fprintf(stderr, "pair selfcheck layer %d %s cmid %d c1 %d cds %d M %lld rc %d/%d: y differs %lld (first px %lld ch %lld), z %lld (first px %lld ch %lld)\n",
+            b.c3.id, wide ? "pairw" : "pair1x1", p.cmid, p.c1, p.cds, M, rc, rc2, dy, fy < 0 ? -1 : fy / p.cexp,
+            fy < 0 ? -1 : fy % p.cexp, dz, fz < 0 ? -1 : fz / p.c1, fz < 0 ? -1 : fz % p.c1);
+  }
+#endif
   return rc;
 }
 

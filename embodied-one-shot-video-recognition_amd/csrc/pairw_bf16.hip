@@ -97,7 +97,7 @@ struct PairW {
 // ops (vmcnt retires loads, stores and LDS-DMA together in issue order, MI355X_MICROARCH.md), so
 // they do not drain the residual prefetch; without CS they count loads only (r03), which is
 // stricter whenever a store is still in flight.
-template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false>
+template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false, int DRAIN = 0>
 __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   using P = PairW<CMID, CEXP, C1, NPT, DSC>;
   const int abl = ABL ? a.abl : 0;
@@ -286,6 +286,7 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
         vm_wait<YOUNG>();
       if (!(abl & 16)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of the slot moves above the barrier (s_barrier is not a compiler memory barrier)
+      if constexpr ((DRAIN & 2) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // profiling: X and everything else have landed
       __builtin_amdgcn_sched_barrier(0);
       // the chunk whose weights this one prefetches (the round's last one(s): the next round's first)
       const int nch = NSLOT == 3 ? (ch + 2 < NCH ? ch + 2 : ch + 2 - NCH) : (ch + 1 < NCH ? ch + 1 : 0);
@@ -351,6 +352,7 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if (gi == XS - 1) {
+          if constexpr ((DRAIN & 1) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // profiling: the residual has landed
           if (u == 3 && cp + 4 == NCH) {  // the round's X is dead: the next round's goes into the same registers
             if (!(abl & 64)) load_x(nxt, rt + gridDim.x, xf);
             __builtin_amdgcn_sched_barrier(0);
@@ -427,10 +429,17 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
 #ifdef EOSV_PROFILING
   static const int abl = env_switch("EOSV_CONV_ABL", 0);
   static const int cs = env_switch("EOSV_PAIRW_CS", CS);  // A/B of the wait rule
+  static const int drain = env_switch("EOSV_PAIRW_DRAIN", 0);  // 1 / 2 / 3: vmcnt(0) before epilogue 1 / after the chunk barrier
   if (abl) {
     Pair1x1Args b = a;
     b.abl = abl;
     hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, true>), dim3((unsigned)grid), dim3(512), 0, s, b);
+  } else if (drain == 1) {
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, false, 1>), dim3((unsigned)grid), dim3(512), 0, s, a);
+  } else if (drain == 2) {
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, false, 2>), dim3((unsigned)grid), dim3(512), 0, s, a);
+  } else if (drain == 3) {
+    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, false, 3>), dim3((unsigned)grid), dim3(512), 0, s, a);
   } else if (cs != CS) {
     hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, !CS>), dim3((unsigned)grid), dim3(512), 0, s, a);
   } else
