@@ -350,12 +350,18 @@ static_assert(12 * (CB_GP - 1) + 12 + 12 <= CB_CH * 16, "ring copy holds every p
 static_assert(2 * (CB_GP - 1) + 1 + 3 < CB_STG, "staged row covers every pair");
 static_assert(4 * CB_GP <= 64 * CB_TILES, "one conversion task per thread");
 
+// AHEAD (r04): the f32 rows of step py + AHEAD are staged at step py.  With AHEAD 1 (r02) every
+// step waited for the HBM round trip of the rows it had staged at its own start (a step's 48
+// MFMAs per wave take ~0.7 us, less than that latency); AHEAD 2 stages into two buffers and
+// waits for the rows staged a step earlier.
+template <int AHEAD>
 __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(const float* __restrict__ fx,
                                                                         const u16* __restrict__ w,
                                                                         const float* __restrict__ bias, u16* y,
                                                                         int H, int W, int Hs, int Ws, int Hq, int Wq) {
-  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 12 * CB_STG * 4];
-  float* stg = (float*)(ring + CB_LDS);  // [row 4][plane 3][CB_STG]
+  static_assert(AHEAD == 1 || AHEAD == 2, "staging depth");
+  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + AHEAD * 12 * CB_STG * 4];
+  float* const stg0 = (float*)(ring + CB_LDS);  // [buffer AHEAD][row 4][plane 3][CB_STG]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: piece addressing on the SALU
@@ -383,7 +389,8 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
   };
   // 4 rows [r0, r0 + 4) x 3 planes -> staging: 12 pieces of 128 floats from column xs0, 3 per
   // wave; 16-B pieces wholly outside the row read column 0 instead (never used: zero padding)
-  auto stage_f32 = [&](int r0) {
+  auto stage_f32 = [&](int r0, int buf) {
+    float* const stg = stg0 + buf * 12 * CB_STG;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int p = wid + CB_TILES * i;
@@ -395,7 +402,8 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
         dma16(fimg + ((long long)c * H + yy) * W + (ok ? xp : 0), stg + (rr * 3 + c) * CB_STG);
     }
   };
-  auto staged_load = [&](int prow, int rr, int g, float (&v)[6]) {
+  auto staged_load = [&](int prow, int rr, int g, int buf, float (&v)[6]) {
+    const float* const stg = stg0 + buf * 12 * CB_STG;
     const int yy = prow - 3;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -468,7 +476,10 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
   // one pooled row: stem rows 2py (into a1) and 2py + 1 (into a2), pooled with `prev` (stem row
   // 2py - 1); the caller rotates the three arrays (no per-step copy of a2 into prev)
   auto step = [&](int py, const f32x4 (&prev)[4], f32x4 (&a1)[4], f32x4 (&a2)[4]) {
-    if (py + 1 < Hq) stage_f32(4 * py + 9);
+    // rows 4 py + 9 .. + 12 are step py + 1's new ones; with AHEAD 2 they were staged at step
+    // py - 1 (step 0: loaded with the first 13 rows) and this step stages step py + 2's
+    if (AHEAD == 1 && py + 1 < Hq) stage_f32(4 * py + 9, 0);
+    if (AHEAD == 2 && py + 2 < Hq) stage_f32(4 * py + 13, py & 1);
     stem_row(2 * py, a1);
     stem_row(2 * py + 1, a2);
     // Pool on the accumulators, which start from the BN shift (max commutes with ReLU and the bf16
@@ -493,12 +504,16 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
         pk4[j][e2] = pack_bf2(o[0], o[1]);
       }
     }
-    if (py + 1 < Hq) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (py + 1 < Hq && (AHEAD == 1 || py >= 1)) {
+      if (AHEAD == 2 && py + 2 < Hq)
+        vm_wait<3>();  // all but this step's 3 staging pieces: the rows staged a step ago have landed
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       if (dtask) {
         float dv[6];
-        staged_load(4 * py + 9 + drow, drow, dg, dv);
+        staged_load(4 * py + 9 + drow, drow, dg, AHEAD == 2 ? (py - 1) & 1 : 0, dv);
         direct_store(4 * py + 9 + drow, dg, dv);
       }
     }
@@ -760,6 +775,14 @@ int launch_stem_pool_x3(const float* frames, int B, int H, int W, const void* w,
   return EOSV_OK;
 }
 
+#ifndef EOSV_STEM_AHEAD_DEF
+#define EOSV_STEM_AHEAD_DEF 2
+#endif
+static int stem_ahead() {
+  static const int v = env_switch("EOSV_STEM_AHEAD", EOSV_STEM_AHEAD_DEF);  // 1 = the r02 one-step staging (A/B switch)
+  return v == 1 ? 1 : 2;
+}
+
 static bool stem_cb() {
   static const bool v = env_switch("EOSV_STEM_CB", 1) != 0;  // 0 = full-width workgroups (A/B switch)
   return v;
@@ -783,11 +806,15 @@ int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, 
     if (B <= 0) return EOSV_OK;
     const int ncb = (ntiles + CB_TILES - 1) / CB_TILES;
     if (info) {
-      static const int occ = kernel_occupancy((const void*)stem_pool_bf16_cb_kernel, 64 * CB_TILES);
+      static const int occ = kernel_occupancy((const void*)stem_pool_bf16_cb_kernel<2>, 64 * CB_TILES);
       return record_launch(info, (long long)B * ncb, occ);
     }
-    hipLaunchKernelGGL(stem_pool_bf16_cb_kernel, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w, bias,
-                       (u16*)y, H, W, Hs, Ws, Hq, Wq);
+    if (stem_ahead() == 1)
+      hipLaunchKernelGGL(stem_pool_bf16_cb_kernel<1>, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w,
+                         bias, (u16*)y, H, W, Hs, Ws, Hq, Wq);
+    else
+      hipLaunchKernelGGL(stem_pool_bf16_cb_kernel<2>, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w,
+                         bias, (u16*)y, H, W, Hs, Ws, Hq, Wq);
     EOSV_LAUNCH_CHECK();
     return EOSV_OK;
   }
