@@ -328,6 +328,9 @@ def main():
         backend = os.environ.get("EOSV_DIST_BACKEND") or "nccl"  # nccl == RCCL on ROCm
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if "MASTER_PORT" not in os.environ:  # N = 1 without a launcher: a free local port
+            if world > 1:  # every rank would pick its own port and the rendezvous would hang
+                sys.exit("bench.py: WORLD_SIZE > 1 needs MASTER_PORT (torch.distributed.run or "
+                         "`bench.py --gpus N` set it)")
             import socket
             with socket.socket() as s:
                 s.bind(("127.0.0.1", 0))

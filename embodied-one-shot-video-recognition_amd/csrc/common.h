@@ -182,7 +182,7 @@ int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
 int launch_pair1x1r_bf16(const Pair1x1Args& a, hipStream_t s);
 // pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
 // streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
-int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128 or 256)
+int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128)
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems);
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv

@@ -61,8 +61,7 @@ __device__ __forceinline__ void dma16(const unsigned char* src, void* lds) {
 // NPT: 16-pixel tiles per wave, 8 waves (two per SIMD); a round is 128 NPT pixels.  The LDS feeds
 // one 1-KiB weight fragment per MFMA at NPT = 1: per 64-channel chunk the 8 waves read 256 KiB
 // (stage 2) / 512 KiB (stage 3) against 1024 / 2048 MFMA cycles per SIMD, i.e. the LDS read
-// rate, not HBM, bounds the pair.  NPT = 2 (r04, the stage-2 pair with C1 = 128: 256-pixel
-// rounds, ~240 VGPRs) reads each fragment once for two pixel tiles.
+// rate, not HBM, bounds the pair.  Only NPT = 1 is built (the static_assert below).
 // DSC > 0 (block 0 of a stage, r03): conv3's K also holds the folded stride-2 1x1 downsample, DSC
 // more columns read from the previous stage's output x2 at pixel (2 oh, 2 ow) (ConvArgs::x2 of
 // the unfused conv), and there is no residual.
@@ -89,6 +88,9 @@ struct PairW {
   static_assert(STAGE_W % (1024 * NW) == 0 && W3B % 1024 == 0 && PPW >= 2, "DMA pieces");
   static_assert(NCH % 4 == 0, "ring slots / residual ring");
   static_assert(PPW < XS + 2 * G2, "DMA pieces go out one per fragment group, the residual loads after them");
+  // NPT 2 (256-pixel rounds) raced inside the backbone for a reason the r04 / r05 evidence did not
+  // pin (see pairw_tile below): it is not built
+  static_assert(NPT == 1, "pairw_bf16: only 16-pixel tiles per wave (128-pixel rounds)");
 };
 
 // ABL (profiling-only instance, EOSV_CONV_ABL bits; results wrong): 1 no weight DMA, 2 no
@@ -97,7 +99,7 @@ struct PairW {
 // ops (vmcnt retires loads, stores and LDS-DMA together in issue order, MI355X_MICROARCH.md), so
 // they do not drain the residual prefetch; without CS they count loads only (r03), which is
 // stricter whenever a store is still in flight.
-template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false, int DRAIN = 0>
+template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false>
 __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   using P = PairW<CMID, CEXP, C1, NPT, DSC>;
   const int abl = ABL ? a.abl : 0;
@@ -249,14 +251,13 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
       // issued after the last piece (order pinned by the sched_barriers) may stay in flight:
       // 2 NPT residual loads (group PPW) and, in the round's last chunk, the next round's XS NPT
       // X loads when the epilogue (after group XS - 1) follows the last piece; before the loop:
-      // XS NPT X loads + 2 RD NPT residual loads after the pieces.  Only loads are counted: vmcnt
-      // retires loads (the DMA included) in order among themselves, but a store can retire ahead
-      // of an older load, so counting the Y / Z stores issued after the last piece as still in
-      // flight let a wave pass with a piece not landed (r03: features of a round changed from run
-      // to run, mostly the tail round's; tools/race_probe.py, conv_check's repeated pairs).  A
-      // store still in flight here only makes the wait stricter (measured: stage-2 pairs 1.43 ->
-      // 1.55 ms, stage-3 0.81 -> 0.87 per 3200 frames; deferring the Y stores by a chunk, to have
-      // them retired by then, gave wrong results and was dropped).
+      // XS NPT X loads + 2 RD NPT residual loads after the pieces.  The default rule (CS, r04)
+      // counts the Y / Z stores issued after the last piece too: vmcnt retires loads, stores and
+      // LDS-DMA in issue order (MI355X_MICROARCH.md), and the r03 failures that had been blamed on
+      // counted stores came from the cp != 0 hole described below.  The r03 loads-only rule
+      // survives only as the CS = 0 A/B instance (EOSV_PAIRW_CS=0, profiling build): a store still
+      // in flight there makes the wait stricter (stage-2 pairs 1.43 -> 1.55 ms, stage-3 0.81 ->
+      // 0.87 per 3200 frames).
       // 3 slots: chunk ch's pieces went out two chunks ago; younger than them are at least that
       // chunk's residual loads and the last chunk's pieces and residual loads (the first two
       // chunks of the launch have more: the prologue's X and residual loads), so the wait no
@@ -286,7 +287,6 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
         vm_wait<YOUNG>();
       if (!(abl & 16)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of the slot moves above the barrier (s_barrier is not a compiler memory barrier)
-      if constexpr ((DRAIN & 2) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // profiling: X and everything else have landed
       __builtin_amdgcn_sched_barrier(0);
       // the chunk whose weights this one prefetches (the round's last one(s): the next round's first)
       const int nch = NSLOT == 3 ? (ch + 2 < NCH ? ch + 2 : ch + 2 - NCH) : (ch + 1 < NCH ? ch + 1 : 0);
@@ -352,7 +352,6 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if (gi == XS - 1) {
-          if constexpr ((DRAIN & 1) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // profiling: the residual has landed
           if (u == 3 && cp + 4 == NCH) {  // the round's X is dead: the next round's goes into the same registers
             if (!(abl & 64)) load_x(nxt, rt + gridDim.x, xf);
             __builtin_amdgcn_sched_barrier(0);
@@ -429,17 +428,10 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
 #ifdef EOSV_PROFILING
   static const int abl = env_switch("EOSV_CONV_ABL", 0);
   static const int cs = env_switch("EOSV_PAIRW_CS", CS);  // A/B of the wait rule
-  static const int drain = env_switch("EOSV_PAIRW_DRAIN", 0);  // 1 / 2 / 3: vmcnt(0) before epilogue 1 / after the chunk barrier
   if (abl) {
     Pair1x1Args b = a;
     b.abl = abl;
     hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, true>), dim3((unsigned)grid), dim3(512), 0, s, b);
-  } else if (drain == 1) {
-    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, false, 1>), dim3((unsigned)grid), dim3(512), 0, s, a);
-  } else if (drain == 2) {
-    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, false, 2>), dim3((unsigned)grid), dim3(512), 0, s, a);
-  } else if (drain == 3) {
-    hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, CS, false, 3>), dim3((unsigned)grid), dim3(512), 0, s, a);
   } else if (cs != CS) {
     hipLaunchKernelGGL((pairw_bf16_kernel<CMID, CEXP, C1, NPT, DSC, !CS>), dim3((unsigned)grid), dim3(512), 0, s, a);
   } else
@@ -449,20 +441,14 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   return EOSV_OK;
 }
 
-// 16-pixel tiles per wave of the pair for this shape: NPT 1 everywhere (the r03 form).  NPT 2 (the
-// stage-2 pair with C1 = 128 on 256-pixel rounds, r04: 1.45 -> 1.34 ms per launch) is off in both
-// builds: in the backbone it gave run-to-run different R50 / R101 features at 64 and 130 frames
-// per chunk (tools/race_modes.py: 4 of 4 plain repeats distinct; 0 with NPT 1), while the same
-// kernel alone, in place and under cold caches and poisoned LDS, stayed bitwise equal to the
-// unfused convs (tests/native/conv_check pairw_stress).  EOSV_PAIRW_NPT2=1 (profiling build)
-// brings it back for study.  NPT 2 fits the register file only without the downsample's 8 extra
-// X fragments (the block-0 pair spills 55 VGPRs at NPT 2) and at C1 = 128.
-static int pairw_npt(int cmid, int c1, int cds) {
-  static const int npt2 = env_switch("EOSV_PAIRW_NPT2", 0);
-  return npt2 && cmid == 128 && c1 == 128 && cds == 0 ? 2 : 1;
-}
-
-int pairw_tile(int cmid, int c1, int cds) { return 128 * pairw_npt(cmid, c1, cds); }
+// One 16-pixel tile per wave (128-pixel rounds) for every shape.  The 256-pixel-round form (NPT 2,
+// r04: the stage-2 pair with C1 = 128, 1.45 -> 1.34 ms per launch) was removed in r05: in the
+// backbone it gave run-to-run different R50 / R101 features at 64, 85 and 130 frames per chunk and
+// none at 17, 37, 257, 601 or 1024, and the recorded evidence did not pin a cause (DESIGN.md
+// section 4: the differing frames map to rounds on every XCD; its ISA has the same wait counts,
+// barrier placement and next-round X load as NPT 1's, and the full-drain and MFMA-fence probes did
+// not remove it).  PairW<...>::NPT is therefore fixed at 1 (static_assert above).
+int pairw_tile(int, int, int) { return 128; }
 
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems) {
   if (M <= 0) return false;
@@ -479,8 +465,7 @@ int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
       (a.cds ? (!a.x2 || a.res || a.Ho <= 0 || a.Wo <= 0 || a.H2 < 2 * a.Ho - 1 || a.W2 < 2 * a.Wo - 1) : (!a.res || a.x2)))
     return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   if (a.cds) return launch_pairw<128, 512, 128, 1, 256>(a, s);
-  if (a.cmid == 128 && a.c1 == 128)
-    return pairw_npt(128, 128, 0) == 2 ? launch_pairw<128, 512, 128, 2>(a, s) : launch_pairw<128, 512, 128, 1>(a, s);
+  if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128, 1>(a, s);
   if (a.cmid == 128) return launch_pairw<128, 512, 256, 1>(a, s);
   return launch_pairw<256, 1024, 256, 1>(a, s);
 }

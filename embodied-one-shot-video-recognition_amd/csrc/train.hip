@@ -2,15 +2,15 @@
 // inference kernels (reference network_train.py:52-131: ResNet in train mode, batch-statistics
 // BN, fc + CrossEntropyLoss, loss.backward(), SGD with momentum on convnet and fc).
 //
-// The conv GEMMs of a training step (forward Y = Xcol . W^T, input gradient dXcol = dY . W,
-// weight gradient dW = dY^T . Xcol) are plain f32 GEMMs over an explicit im2col buffer
-// (288 GB of HBM holds the largest, R50 stem at 96 frames: 0.8 GB), so they go to rocBLAS
-// (atomics off: deterministic).  Everything around them is here: im2col / col2im (gather,
+// The conv GEMMs of a training step that are not the inference conv kernels' shape (the stem's
+// forward over an explicit im2col buffer -- 288 GB of HBM holds the largest, R50 stem at 96
+// frames: 0.8 GB --, strided-conv input gradients dXcol = dY . W, 1x1 / stem weight gradients
+// dW = dY^T . Xcol, the fc) are plain f32 GEMMs on the in-tree exact-f32 MFMA kernel
+// (gemm_f32.hip, deterministic split-K; rocBLAS until r04).  Everything around them is here: im2col / col2im (gather,
 // deterministic), batch-norm forward with batch statistics and running-stat update, its
 // backward with the ReLU mask and the residual branch fused, max-pool with argmax indices and
 // its gather backward, average pool, softmax cross-entropy, SGD with momentum.
 // Layouts: activations NHWC f32 ([P][C] rows, P = N*H*W), conv weights [Cout][KH][KW][Cin].
-#include <rocblas/rocblas.h>
 
 #include <mutex>
 
@@ -521,13 +521,6 @@ __global__ void sum_rows_kernel(const float* __restrict__ x, int rows, int C, fl
 }
 
 // C[i] = sum over the slices of W (fixed slice order: deterministic)
-__global__ void sum_slices_kernel(const float* __restrict__ w, int slices, long long mn, float* __restrict__ c) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < mn; i += (long long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int j = 0; j < slices; ++j) s += w[j * mn + i];
-    c[i] = s;
-  }
-}
 
 __global__ void add_bias_kernel(float* __restrict__ y, int rows, int C, const float* __restrict__ b) {
   const long long total = (long long)rows * C;
@@ -594,19 +587,6 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, i
   }
 }
 
-// one rocBLAS handle per device (created on first use, never destroyed: lives with the process)
-rocblas_handle blas_handle(int dev) {
-  static std::mutex mu;
-  static rocblas_handle hs[64] = {};
-  std::lock_guard<std::mutex> lk(mu);
-  if (dev < 0 || dev >= 64) return nullptr;
-  if (!hs[dev]) {
-    if (rocblas_create_handle(&hs[dev]) != rocblas_status_success) return hs[dev] = nullptr;
-    rocblas_set_atomics_mode(hs[dev], rocblas_atomics_not_allowed);
-  }
-  return hs[dev];
-}
-
 bool pos(long long v) { return v > 0; }
 }  // namespace
 }  // namespace eosv
@@ -614,74 +594,6 @@ bool pos(long long v) { return v > 0; }
 using namespace eosv;
 
 extern "C" {
-
-int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* d_a, int lda,
-               const float* d_b, int ldb, float beta, float* d_c, int ldc, eosv_stream_t stream) {
-  if (m < 0 || n < 0 || k < 0 || !d_c || (k > 0 && (!d_a || !d_b)) || lda <= 0 || ldb <= 0 || ldc < n)
-    return set_error("eosv_sgemm: bad argument"), EOSV_ERR_ARG;
-  if (m == 0 || n == 0) return EOSV_OK;
-  int dev = 0;
-  EOSV_HIP_CHECK(hipGetDevice(&dev));
-  rocblas_handle h = blas_handle(dev);
-  if (!h) return set_error("eosv_sgemm: rocblas_create_handle failed"), EOSV_ERR_HIP;
-  rocblas_set_stream(h, (hipStream_t)stream);
-  // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T on the same buffers
-  const rocblas_status st =
-      rocblas_sgemm(h, trans_b ? rocblas_operation_transpose : rocblas_operation_none,
-                    trans_a ? rocblas_operation_transpose : rocblas_operation_none, n, m, k, &alpha, d_b, ldb, d_a,
-                    lda, &beta, d_c, ldc);
-  if (st != rocblas_status_success)
-    return set_error(std::string("eosv_sgemm: ") + rocblas_status_to_string(st)), EOSV_ERR_HIP;
-  return EOSV_OK;
-}
-
-// split-K plan of C = A^T B: enough slices that the rocBLAS tiles x slices fill the chip,
-// each slice at least 256 reduction rows
-static int splitk_slices(int m, int n, int k) {
-  const long long tiles = (long long)((m + 63) / 64) * ((n + 255) / 256);
-  const long long target = env_switch("EOSV_SPLITK_TARGET", 256);
-  long long s = (target + tiles - 1) / tiles;
-  s = std::min<long long>(s, std::max(1, k / env_switch("EOSV_SPLITK_MINROWS", 2048)));
-  return (int)std::max<long long>(1, std::min<long long>(s, 256));
-}
-
-int64_t eosv_sgemm_tn_splitk_workspace(int m, int n, int k) {
-  if (m <= 0 || n <= 0 || k <= 0) return 0;
-  const int s = splitk_slices(m, n, k);
-  return s > 1 ? (int64_t)s * m * n * (int64_t)sizeof(float) : 0;
-}
-
-int eosv_sgemm_tn_splitk(int m, int n, int k, const float* d_a, int lda, const float* d_b, int ldb, float* d_c,
-                         int ldc, float* d_work, int64_t work_bytes, eosv_stream_t stream) {
-  if (m <= 0 || n <= 0 || k <= 0 || !d_a || !d_b || !d_c || lda < m || ldb < n || ldc != n)
-    return set_error("eosv_sgemm_tn_splitk: bad argument"), EOSV_ERR_ARG;
-  const int want = splitk_slices(m, n, k);
-  if (want == 1 || work_bytes < eosv_sgemm_tn_splitk_workspace(m, n, k) || !d_work)
-    return eosv_sgemm(1, 0, m, n, k, 1.f, d_a, lda, d_b, ldb, 0.f, d_c, ldc, stream);
-  int dev = 0;
-  EOSV_HIP_CHECK(hipGetDevice(&dev));
-  rocblas_handle h = blas_handle(dev);
-  if (!h) return set_error("eosv_sgemm_tn_splitk: rocblas_create_handle failed"), EOSV_ERR_HIP;
-  rocblas_set_stream(h, (hipStream_t)stream);
-  const int kc = (k + want - 1) / want;
-  const int full = k / kc, rem = k - full * kc;
-  const long long mn = (long long)m * n;
-  const float one = 1.f, zero = 0.f;
-  // slice j: W_j^T (n x m, column-major) = B_j (n x kc) . A_j^T, A_j / B_j = rows j*kc.. of A / B
-  rocblas_status st = rocblas_sgemm_strided_batched(
-      h, rocblas_operation_none, rocblas_operation_transpose, n, m, kc, &one, d_b, ldb, (long long)kc * ldb, d_a, lda,
-      (long long)kc * lda, &zero, d_work, n, mn, full);
-  if (st == rocblas_status_success && rem > 0)
-    st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, n, m, rem, &one,
-                       d_b + (long long)full * kc * ldb, ldb, d_a + (long long)full * kc * lda, lda, &zero,
-                       d_work + full * mn, n);
-  if (st != rocblas_status_success)
-    return set_error(std::string("eosv_sgemm_tn_splitk: ") + rocblas_status_to_string(st)), EOSV_ERR_HIP;
-  hipLaunchKernelGGL(sum_slices_kernel, dim3(grid_for(mn)), dim3(256), 0, (hipStream_t)stream, d_work,
-                     full + (rem > 0), mn, d_c);
-  EOSV_LAUNCH_CHECK();
-  return EOSV_OK;
-}
 
 int eosv_im2col(const float* d_x, int N, int H, int W, int C, int KH, int KW, int stride, int pad, float* d_col,
                 eosv_stream_t stream) {

@@ -16,10 +16,10 @@ LIB_PATH = os.environ.get("EOSV_LIBRARY") or os.path.join(PKG_ROOT, "libeosv.so"
 
 def source_digest() -> str:
     """sha256 (16 hex) of the library's sources and build recipe (csrc/*.hip, common.h,
-    include/eosv.h, csrc/Makefile) plus the build-configuring environment (HIPCC flags and any
-    EOSV_* compile macro given through CXXFLAGS / EXTRA_FLAGS): ties a profile (e.g.
-    profiles/*_traffic.json) to the kernels it measured; computable on the GPU box, where there is
-    no git history."""
+    include/eosv.h, csrc/Makefile) and of the bytes of the library this process loads (LIB_PATH:
+    libeosv.so, or the EOSV_LIBRARY build): ties a profile (e.g. profiles/*_traffic.json) to the
+    kernels it measured, so a profiling or variant build never passes for the release one;
+    computable on the GPU box, where there is no git history."""
     import glob
     import hashlib
 
@@ -32,10 +32,10 @@ def source_digest() -> str:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
-    for k in ("CXXFLAGS", "EXTRA_FLAGS", "HIPCC", "ARCH"):
-        v = os.environ.get(k)
-        if v:
-            h.update(f"{k}={v}".encode())
+    h.update(b"library:")
+    if os.path.exists(LIB_PATH):
+        with open(LIB_PATH, "rb") as fh:
+            h.update(fh.read())
     return h.hexdigest()[:16]
 
 

@@ -194,7 +194,7 @@ class NativeTrainer:
         Ho, Wo = (H + 2 * c.pad - c.k) // c.stride + 1, (W + 2 * c.pad - c.k) // c.stride + 1
         P = N * Ho * Wo
         y = torch.empty(P * c.cout, dtype=torch.float32, device=self.dev)
-        # the inference conv kernels (exact-f32 MFMA) where they apply, else im2col + rocBLAS
+        # the inference conv kernels (exact-f32 MFMA) where they apply, else im2col + the in-tree GEMM
         kb = int(self.L.eosv_conv2d_f32_workspace(N, H, W, c.cin, c.cout, c.k, c.k, c.stride, c.pad))
         kw = self._buf("ksplit", kb // 4 + 4)
         rc = self.L.eosv_conv2d_f32(_f(x), N, H, W, c.cin, _f(c.w), c.cout, c.k, c.k, c.stride, c.pad, None, None, 0,
@@ -221,8 +221,7 @@ class NativeTrainer:
         rc = _UNSUPPORTED
         if c.cin % 4 == 0 and not direct:
             # KxK and strided 1x1: implicit-GEMM weight gradient (no im2col buffer).  Stride-1 1x1
-            # convs stay on rocBLAS (X is already the GEMM operand; measured faster on 9 of the 11
-            # R50 shapes, tools/bench_train_convs.py)
+            # convs take the plain split-K GEMM (X is already its operand: gemm_f32.hip TN)
             wb = int(self.L.eosv_conv_wgrad_f32_workspace(N, H, W, c.cin, c.cout, c.k, c.k, c.stride, c.pad))
             ws = self._buf("splitk", wb // 4 + 4)
             rc = self.L.eosv_conv_wgrad_f32(_f(x), N, H, W, c.cin, _f(dz), c.cout, c.k, c.k, c.stride, c.pad, _f(c.g),

@@ -1,7 +1,7 @@
 """Drop-in for the reference's ``network_train.py`` (TrainNetwork, lines 21-131).
 
 Same constructor, ``finetune_model(data_aug, pre_model)`` semantics and loss-file format; the
-step itself runs natively (eosv.train.NativeTrainer over csrc/train.hip and rocBLAS): ResNet in
+step itself runs natively (eosv.train.NativeTrainer over csrc/train.hip and csrc/gemm_f32.hip): ResNet in
 train mode with batch-statistics BN, the clip mean over T frames (:100, :110), fc,
 CrossEntropyLoss, backward, SGD(momentum=0.9) with lr_1 on the convnet and lr_2 on the fc, and
 StepLR(step_size, gamma=0.1) stepped at the start of every epoch as the reference does (:83-84:

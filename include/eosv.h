@@ -153,7 +153,10 @@ int eosv_synth_frames(const uint64_t* d_params, int n_frames, int H, int W, floa
  * 0 = stem, then each block's convs in order, fc last).  eosv_profile_read
  * synchronises on the recorded events and returns, per layer id < max_layers,
  * the summed milliseconds, summed algorithmic FLOPs (2 x MACs) and launch count;
- * the return value is the number of layer ids in the plan.  Enabling clears the log. */
+ * the return value is the number of layer ids in the plan.  Enabling clears the log.
+ * Switching it on / off also launches one empty marker kernel on the null stream
+ * (profile_window_begin_kernel / profile_window_end_kernel), so that a rocprofv3 trace or PMC
+ * pass of the same run can select exactly the window's dispatches. */
 int eosv_profile_enable(eosv_handle* h, int enable);
 int eosv_profile_read(eosv_handle* h, double* ms, double* flops, int64_t* launches, int max_layers);
 
@@ -184,16 +187,19 @@ int eosv_backbone_probe(eosv_handle* h, const float* d_frames, int B, int stage,
  * Python trainer (eosv/train.py) chains these f32 kernels; activations NHWC ([P][C] rows),
  * conv weights [Cout][KH][KW][Cin].  No handle: every call is stateless on caller buffers. */
 
-/* Row-major C[m][n] = alpha * op(A) op(B) + beta * C (op = transpose when trans_*), rocBLAS
- * sgemm with atomics disabled (deterministic).  The conv GEMMs of a training step: forward
- * Y = Xcol W^T (models.py:19 in train mode), input gradient dXcol = dY W and weight gradient
- * dW = dY^T Xcol (loss.backward(), network_train.py:114). */
+/* Row-major C[m][n] = alpha * op(A) op(B) + beta * C (op = transpose when trans_*; beta 0: C is
+ * not read) on the in-tree exact-f32 MFMA GEMM (gemm_f32.hip; deterministic, no atomics).  The
+ * conv GEMMs of a training step that are not the inference conv kernels' shape: the stem's
+ * forward Y = Xcol W^T (models.py:19 in train mode), strided-conv input gradients dXcol = dY W,
+ * 1x1 / stem weight gradients dW = dY^T Xcol (loss.backward(), network_train.py:114), and the fc
+ * (logits, its weight and input gradients).  Replaced rocBLAS sgemm in r05. */
 int eosv_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha, const float* d_a, int lda,
                const float* d_b, int ldb, float beta, float* d_c, int ldc, eosv_stream_t stream);
 /* Weight-gradient GEMM C[m][n] = A^T B with A [k][m], B [k][n] row-major and k (the pixel count
- * P of a conv) much larger than m, n: the reduction is split into slices, each a strided-batched
- * rocBLAS GEMM into d_work, then summed in a fixed order (deterministic).  work_bytes below
- * eosv_sgemm_tn_splitk_workspace(m, n, k) falls back to one eosv_sgemm.  ldc must equal n. */
+ * P of a conv) much larger than m, n: the reduction is split into slices (one workgroup grid
+ * dimension), each writing its partial tile to d_work, then summed in slice order
+ * (deterministic).  work_bytes below eosv_sgemm_tn_splitk_workspace(m, n, k) runs one slice.
+ * ldc must equal n. */
 int64_t eosv_sgemm_tn_splitk_workspace(int m, int n, int k);
 int eosv_sgemm_tn_splitk(int m, int n, int k, const float* d_a, int lda, const float* d_b, int ldb, float* d_c,
                          int ldc, float* d_work, int64_t work_bytes, eosv_stream_t stream);

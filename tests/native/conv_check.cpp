@@ -538,7 +538,7 @@ static int check_pairw(int N, int H, int W, int cmid, int cexp, int c1, int cds 
   auto fill = [&](std::vector<unsigned short>& v, float scale) {
     for (auto& e : v) e = f2bf(frand(s) * scale);
   };
-  const long long tile = pairw_tile(cmid, c1, cds);  // 128 or 256 pixels per round
+  const long long tile = pairw_tile(cmid, c1, cds);  // 128 pixels per round
   const long long Mp = (M + tile - 1) / tile * tile;  // padded to whole rounds
   std::vector<unsigned short> x(Mp * cmid, 0x7fc0), res(Mp * cexp, 0x7fc0), w3((size_t)cexp * K3), w1((size_t)c1 * cexp);
   std::vector<unsigned short> x2(cds ? (size_t)N * H2 * W2 * cds : 1);

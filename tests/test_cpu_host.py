@@ -36,6 +36,21 @@ def test_cabi_library_exports_every_header_symbol():
     assert set(syms) == set(_lib.EXPORTS)
 
 
+def test_cabi_library_links_no_vendor_blas():
+    """Every GEMM of the path (inference convs, training GEMMs since r05) is an in-tree kernel: the
+    library's dynamic section names no rocBLAS / hipBLAS(Lt) / MIOpen."""
+    import subprocess
+
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    dyn = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", dyn)
+    assert needed, dyn
+    bad = [n for n in needed if re.search(r"blas|miopen|hipblaslt", n, re.I)]
+    assert not bad, needed
+
+
 def test_cabi_null_arguments_fail_cleanly():
     L = _lib.lib()
     assert L.eosv_create(None, None) == -1

@@ -172,6 +172,70 @@ def _call(fn, *args):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k,pad,alpha,beta", [
+    (6, 64, 2048, 0, 1.0, 0.0),      # fc logits / input gradient shapes
+    (64, 2048, 6, 0, 1.0, 0.0),      # fc weight gradient (k = batch)
+    (301, 147, 77, 0, 1.0, 0.0),     # stem-like: ragged m, n and k not multiples of 4 or 16
+    (256, 192, 320, 3, 0.5, -2.0),   # padded leading dimensions (scalar path), alpha / beta
+    (1000, 128, 256, 0, 1.0, 1.0)])  # several tiles, accumulate into C
+def test_sgemm_in_tree_vs_torch(ta, tb, m, n, k, pad, alpha, beta):
+    """eosv_sgemm (gemm_f32.hip, exact-f32 MFMA, in place of rocBLAS since r05) for every
+    transpose pair against torch f64 matmul: C = alpha op(A) op(B) + beta C, row-major, with
+    ragged edges and padded leading dimensions; 1e-5 relative.  Bitwise deterministic over runs."""
+    from eosv._lib import lib
+
+    L = lib()
+    g = torch.Generator().manual_seed(m * 7 + n + k)
+    ar, ac = (k, m) if ta else (m, k)
+    br, bc = (n, k) if tb else (k, n)
+    A = torch.randn(ar, ac + pad, generator=g, dtype=torch.float64)
+    B = torch.randn(br, bc + pad, generator=g, dtype=torch.float64)
+    C0 = torch.randn(m, n + pad, generator=g, dtype=torch.float64)
+    opA = A[:, :ac].T if ta else A[:, :ac]
+    opB = B[:, :bc].T if tb else B[:, :bc]
+    ref = alpha * (opA @ opB) + beta * C0[:, :n]
+    Ad, Bd = A.float().cuda(), B.float().cuda()
+    outs = []
+    for _ in range(2):
+        Cd = C0.float().cuda()
+        _call(L.eosv_sgemm, ta, tb, m, n, k, alpha, Ad.data_ptr(), ac + pad, Bd.data_ptr(), bc + pad, beta,
+              Cd.data_ptr(), n + pad)
+        outs.append(Cd)
+    assert torch.equal(outs[0], outs[1])
+    got = outs[0][:, :n].double().cpu()
+    assert float((got - ref).norm() / ref.norm()) < 1e-5
+    assert torch.equal(outs[0][:, n:].cpu(), C0[:, n:].float())  # padding columns untouched
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 64, 100352), (64, 147, 37632 + 5), (2048, 1024, 4704)])
+def test_sgemm_tn_splitk_vs_torch(m, n, k):
+    """The split-K weight-gradient GEMM C = A^T B (reduction over the pixel count, slices summed in
+    order) against torch f64: 1e-5 relative, bitwise equal over runs, and equal to the one-slice
+    result within 1e-5 (a different summation split)."""
+    from eosv._lib import lib
+
+    L = lib()
+    g = torch.Generator().manual_seed(k)
+    A = torch.randn(k, m, generator=g, dtype=torch.float64)
+    B = torch.randn(k, n, generator=g, dtype=torch.float64)
+    ref = A.T @ B
+    Ad, Bd = A.float().cuda(), B.float().cuda()
+    wb = int(L.eosv_sgemm_tn_splitk_workspace(m, n, k))
+    assert wb > 0
+    ws = torch.empty(wb // 4 + 4, device="cuda")
+    outs = []
+    for _ in range(2):
+        C = torch.empty(m, n, device="cuda")
+        _call(L.eosv_sgemm_tn_splitk, m, n, k, Ad.data_ptr(), m, Bd.data_ptr(), n, C.data_ptr(), n, ws.data_ptr(), wb)
+        outs.append(C)
+    assert torch.equal(outs[0], outs[1])
+    assert float((outs[0].double().cpu() - ref).norm() / ref.norm()) < 1e-5
+    one = torch.empty(m, n, device="cuda")
+    _call(L.eosv_sgemm_tn_splitk, m, n, k, Ad.data_ptr(), m, Bd.data_ptr(), n, one.data_ptr(), n, ws.data_ptr(), 0)
+    assert float((one - outs[0]).norm() / outs[0].norm()) < 1e-5
+
+
 @pytest.mark.parametrize("k,stride,pad,cin,cout", [(3, 1, 1, 8, 16), (3, 2, 1, 8, 16), (1, 2, 0, 16, 8), (7, 2, 3, 3, 8)])
 def test_conv_forward_and_gradients_vs_torch(k, stride, pad, cin, cout):
     """im2col + eosv_sgemm forward, weight gradient and col2im input gradient against torch

@@ -85,41 +85,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
 if bench:
     open(f"{dst}/{tag}_bench.json", "w").write(json.dumps(bench) + "\n")
 
-# conv-family HBM traffic per launch (read by bench.py into roofline.traffic)
-FAMILIES = {"f32": ("conv_f32",), "bf16": ("conv_bf16", "conv_rows_bf16", "stem_pool_bf16", "pair1x1_bf16"),
-            "f32x3": ("conv_bf16", "stem_pool_x3")}
-
-
-def split_kernel(k):
-    """EOSV_F32X3 launches: the bf16 conv templates instantiated with SPLIT = true (their last
-    template argument) and the split-bf16 stem."""
-    return "stem_pool_x3" in k or (k.startswith("conv_bf16") and k.rstrip().endswith("true>"))
-traffic = {"source": f"profiles/{tag}_pmc_FETCH_SIZE.csv + profiles/{tag}_pmc_WRITE_SIZE.csv "
-                     "(rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes of "
-                     "`bench.py --no-cpu-baseline --steps 2`)",
-           "formula": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per launch, averaged over the conv family "
-                      "(gfx950: FETCH_SIZE counts half of wide coalesced reads; MI355X_MICROARCH.md HBM)"}
-for fam, keys in FAMILIES.items():
-    tot = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
-    n = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
-    for k in pmc:
-        if any(key in k for key in keys) and split_kernel(k) == (fam == "f32x3"):
-            for c in tot:
-                tot[c] += pmc[k][c]
-                n[c] += cnt[k][c]
-    if n["FETCH_SIZE"] and n["WRITE_SIZE"]:
-        traffic[fam] = {"launches": n["FETCH_SIZE"],
-                        "hbm_bytes_per_launch": round((2 * tot["FETCH_SIZE"] / n["FETCH_SIZE"] +
-                                                       tot["WRITE_SIZE"] / n["WRITE_SIZE"]) * 1024)}
-if bench:  # the workload these counters belong to (bench.py attaches them only to the same one)
-    import re
-    mm = re.search(r"(resnet\d+), (\d+)x(\d+)", bench["config"]["workload"])
-    if mm:
-        traffic["key"] = f"{mm.group(1)}@{mm.group(2)}x{mm.group(3)}"
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                "embodied-one-shot-video-recognition_amd"))
-from eosv._lib import source_digest  # noqa: E402
-
-traffic["src_sha16"] = source_digest()  # bench.py attaches these counters only to the same kernels
-open(f"{dst}/{tag}_traffic.json", "w").write(json.dumps(traffic, indent=1) + "\n")
+# HBM traffic (roofline.traffic) is written by tools/traffic_json.py from PMC passes over the
+# library's profiling window (tools/gpu_traffic.sh), not here: whole-run counters mix warmup and
+# setup dispatches into the figure
 print("\n".join(out))
