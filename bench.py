@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
     ap.add_argument("--config-label", default="BASELINE configs[1]",
                     help="which BASELINE.json config this run measures (tools/bench_configs.py sets it)")
+    ap.add_argument("--parity-dump", default=None,
+                    help="save the primary leg's timed-episode predictions and clip embeddings (npz) for "
+                         "tools/offline_parity.py (the oracle over many more episodes than cpu_parity's sample)")
     ap.add_argument("--secondary-dtype", default="bf16,f32x3",
                     help="also time the same episodes with these backbone dtypes, comma-separated "
                          "('' or none to skip); the first is reported as 'secondary', the others as "
@@ -126,9 +129,10 @@ def cpu_baseline(args, batch, T, emb, preds):
     return base, parity
 
 
-def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
+def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist, keep_emb=False):
     """Warmup + timed region for one backbone dtype; returns (max-over-ranks elapsed_s, every rank's
-    elapsed_s, preds, per-layer profile, clip embeddings of the last step)."""
+    elapsed_s, preds, per-layer profile, clip embeddings of the last step; with keep_emb those of
+    every timed step, concatenated)."""
     bb = engine.Backbone(args.arch, dtype, args.res, args.res, max_frames=args.max_frames, device=local)
     bb.load_state_dict(synth.synth_state_dict(arch_mod.SPECS[args.arch], 64, 0))
     feat = torch.empty(max(d.batch.n_frames for d in batches), bb.D, device=f"cuda:{local}")
@@ -140,12 +144,14 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     bb.profile(True)
-    preds = []
+    preds, embs = [], []
     t0 = time.perf_counter()
     for s in range(args.warmup, len(batches)):
         d = batches[s]
         p, emb, _ = engine.run_episodes(bb, d, "protonet", True, feat=feat[:d.batch.n_frames])
         preds.append(p)
+        if keep_emb:
+            embs.append(emb.clone())  # the next step reuses the output buffer
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -156,6 +162,8 @@ def run_timed(args, engine, arch_mod, synth, batches, dtype, local, dist):
     bb.close()
     from eosv import dist as edist
     per_rank = edist.gather_values(elapsed)
+    if keep_emb:
+        return max(per_rank), per_rank, torch.cat(preds), prof, torch.cat(embs).cpu().numpy()
     return max(per_rank), per_rank, torch.cat(preds), prof, emb.cpu().numpy()
 
 
@@ -352,7 +360,15 @@ def main():
     torch.cuda.synchronize()
     timed_idx = mine_idx[args.warmup * E:]
 
-    elapsed, per_rank_elapsed, pred, prof, emb = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist)
+    dump = bool(args.parity_dump) and world == 1
+    elapsed, per_rank_elapsed, pred, prof, emb = run_timed(args, engine, arch_mod, synth, batches, args.dtype, local, dist,
+                                                           keep_emb=dump)
+    if dump:  # every timed step's embeddings: the last step's are the tail (cpu_baseline's sample)
+        all_emb = emb
+        emb = all_emb[-batches[-1].batch.n_clips:]
+        np.savez_compressed(args.parity_dump, pred=pred.cpu().numpy().astype(np.int64), emb=all_emb,
+                            timed_idx=np.asarray(timed_idx, np.int64), n_plans=len(plans),
+                            args=json.dumps({k: v for k, v in vars(args).items()}))
     per_rank_clips = [int(v) for v in edist.gather_values(sum(d.batch.n_clips for d in batches[args.warmup:]))]
     clips = sum(per_rank_clips)
     frames_rank = sum(d.batch.n_frames for d in batches[args.warmup:])

@@ -331,7 +331,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
 // (EPI_LDS): bit-identical outputs.  Inference only (no split-K), tap-major or chunk-major K.
 // OCC: workgroups per CU the register budget is sized for (2 at NP 4: <= 80 VGPRs, 6 waves per SIMD;
 // 2 at NP 2: <= 96)
-template <int BM, int BN, int WM, int WN, int NP, bool DS, int OCC>
+// EPD (r05 A/B, EOSV_F32_EPD): the epilogue straight from the accumulators, no LDS staging and no
+// barriers: a 32 x 32 accumulator register is 2 rows x 32 consecutive channels, i.e. two whole
+// 128-B lines per wave instruction for the residual load and the store.
+template <int BM, int BN, int WM, int WN, int NP, bool DS, int OCC, bool EPD = false>
 __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4) void conv_f32_ws_kernel(ConvArgs a) {
   constexpr int BK = 16, CPR = BK / 4, RPI = 64 / CPR, RPB = 64 / BK;
   constexpr int NW = WM * WN;
@@ -511,6 +514,32 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
     const int n = n0 + wn * (BN / WN) + j * 32 + r;
     bcol[j] = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
   }
+  if constexpr (EPD) {
+    // same arithmetic order as the staged epilogue: (acc + bias) + residual, then ReLU
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * (BN / WN) + j * 32 + r;
+        if (n >= a.Cout) continue;
+        float rv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm * (BM / WM) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+          rv[q] = (res && m < M) ? res[(long long)m * a.Cout + n] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm * (BM / WM) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+          if (m >= M) continue;
+          float v = acc[i][j][q] + bcol[j];
+          if (res) v += rv[q];
+          if (a.relu) v = fmaxf(v, 0.f);
+          y[(long long)m * a.Cout + n] = v;
+        }
+      }
+    return;
+  }
   float* ep = smem;
   constexpr int nthreads = 64 * NW;
 #pragma unroll
@@ -640,6 +669,19 @@ static int launch_ws(const ConvArgs& a, hipStream_t s) {
     static const int occ = kernel_occupancy((const void*)conv_f32_ws_kernel<BM, BN, WM, WN, NP, false, OCC>, NT);
     return record_launch(a.plan, nb, occ);
   }
+#ifdef EOSV_PROFILING
+  static const int epd = env_switch("EOSV_F32_EPD", 0);  // 1: epilogue from registers (A/B)
+  if (epd) {
+    if (a.x2) {
+      if (a.K1 % 16 || a.Cin2 % 16) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
+      hipLaunchKernelGGL((conv_f32_ws_kernel<BM, BN, WM, WN, NP, true, OCC, true>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((conv_f32_ws_kernel<BM, BN, WM, WN, NP, false, OCC, true>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+    }
+    EOSV_LAUNCH_CHECK();
+    return EOSV_OK;
+  }
+#endif
   if (a.x2) {
     if (a.K1 % 16 || a.Cin2 % 16) return set_error("conv_f32: fused downsample shape"), EOSV_ERR_UNSUPPORTED;
     hipLaunchKernelGGL((conv_f32_ws_kernel<BM, BN, WM, WN, NP, true, OCC>), dim3((unsigned)nb), dim3(NT), 0, s, a);

@@ -202,16 +202,48 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
     }
 }
 
-// C[m][n] = alpha * sum over slices (in slice order) of w[s][m][n] + beta * C
+// C[m][n] = alpha * sum over slices (in slice order) of w[s][m][n] + beta * C; 4 consecutive
+// elements per thread (n % 4 == 0: one float4 per slice), 8 slices' loads in flight before their
+// adds (the adds stay in slice order)
+template <bool V4>
 __global__ void gemm_slice_sum_kernel(const float* __restrict__ w, int slices, int m, int n, float alpha, float beta,
                                       float* __restrict__ c, long long ldc) {
   const long long mn = (long long)m * n;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < mn; i += (long long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int j = 0; j < slices; ++j) s += w[j * mn + i];
-    const long long r = i / n, col = i - r * n;
-    float* o = c + r * ldc + col;
-    *o = beta != 0.f ? alpha * s + beta * *o : alpha * s;
+  for (long long i = 4 * (blockIdx.x * (long long)blockDim.x + threadIdx.x); i < mn;
+       i += 4 * (long long)gridDim.x * blockDim.x) {
+    f32x4 s{0.f, 0.f, 0.f, 0.f};
+    int j = 0;
+    for (; j + 8 <= slices; j += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float* p = w + (j + u) * mn + i;
+        if (V4) {
+          v[u] = *(const f32x4*)p;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[u][e] = i + e < mn ? p[e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; j < slices; ++j) {
+      const float* p = w + j * mn + i;
+      if (V4) {
+        s += *(const f32x4*)p;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] += i + e < mn ? p[e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (i + e >= mn) break;
+      const long long r = (i + e) / n, col = (i + e) - r * n;
+      float* o = c + r * ldc + col;
+      *o = beta != 0.f ? alpha * s[e] + beta * *o : alpha * s[e];
+    }
   }
 }
 
@@ -220,8 +252,9 @@ struct GemmPlan {
 };
 
 // tile: 128 x 128 (2 x 2 waves) when both dimensions reach 128, else the 64-wide side where one
-// is short (64 x 128, 128 x 64, 64 x 64); split-K (when allowed) so that tiles x slices is about 4
-// workgroups per CU with at least 256 reduction rows per slice
+// is short (64 x 128, 128 x 64, 64 x 64); split-K (when allowed) so that tiles x slices is about 2
+// workgroups per CU with at least 1024 reduction rows per slice and at most 256 slices (the
+// slice sum re-reads slices x m x n floats)
 GemmPlan gemm_plan(int m, int n, int k, bool split) {
   GemmPlan p{};
   p.wm = m > 64 ? 2 : 1;
@@ -231,9 +264,9 @@ GemmPlan gemm_plan(int m, int n, int k, bool split) {
   const long long tiles = (long long)p.mt * p.nt;
   long long s = 1;
   if (split) {
-    const long long target = 4LL * device_cu_count();
-    s = std::max(1LL, std::min((target + tiles - 1) / tiles, (long long)k / 256));
-    s = std::min<long long>(s, 1024);
+    const long long target = 2LL * device_cu_count();
+    s = std::max(1LL, std::min((target + tiles - 1) / tiles, (long long)k / 1024));
+    s = std::min<long long>(s, 256);
   }
   long long kps = (k + s - 1) / s;
   if (s > 1) kps = (kps + GB_K - 1) / GB_K * GB_K;
@@ -283,8 +316,11 @@ int launch_gemm(bool ta, bool tb, int m, int n, int k, float alpha, const float*
   EOSV_LAUNCH_CHECK();
   if (g.partial) {
     const long long mn = (long long)m * n;
-    hipLaunchKernelGGL(gemm_slice_sum_kernel, dim3((unsigned)std::min<long long>((mn + 255) / 256, 1 << 16)), dim3(256),
-                       0, s, work, p.slices, m, n, alpha, beta, c, ldc);
+    const dim3 sg((unsigned)std::min<long long>((mn / 4 + 255) / 256 + 1, 1 << 16));
+    if (n % 4 == 0)
+      hipLaunchKernelGGL(gemm_slice_sum_kernel<true>, sg, dim3(256), 0, s, work, p.slices, m, n, alpha, beta, c, ldc);
+    else
+      hipLaunchKernelGGL(gemm_slice_sum_kernel<false>, sg, dim3(256), 0, s, work, p.slices, m, n, alpha, beta, c, ldc);
     EOSV_LAUNCH_CHECK();
   }
   return EOSV_OK;

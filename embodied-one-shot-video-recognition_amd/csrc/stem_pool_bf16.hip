@@ -36,6 +36,8 @@
 
 #include "common.h"
 
+#include <type_traits>
+
 namespace eosv {
 
 namespace {
@@ -541,6 +543,247 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb_kernel(con
 }
 
 
+// r05 form of the column-blocked DIRECT kernel (default; EOSV_STEM_V5=0 selects the r04 one):
+// the same tiles, ring, staging and arithmetic (bitwise equal outputs), with the per-step issue
+// cost cut, since the SIMD's vector issue -- not the MFMA pipe -- bounded the r04 loop (SQ:
+// MFMA-busy 0.39, ~155 VALU + 48 MFMA per wave-step, r04j_sq_r18_bf16.txt):
+//  * ONE barrier per step, at its top: it covers the previous step's ring writes (lgkmcnt(0)) and
+//    the previous step's staging DMA (each wave waits for its own pieces with vmcnt(4): the step's
+//    4 output stores are the only younger memory ops, and every wave issues exactly 4 -- buffer
+//    stores, non-writers out of range -- so the count holds for every wave), and it orders the
+//    previous step's ring / staging reads before this step's overwrites;
+//  * the step loop is unrolled by 12 (the ring's 4-step period x the 3-way accumulator rotation),
+//    so every ring address is a per-lane register + a compile-time offset: no VALU address math
+//    (36 VALU per wave-step in r04).  The ring wrap inside a step's 9-row window is a second
+//    per-lane register (for the k-slices whose two kernel rows straddle slot 15 -> 0);
+//  * out-of-frame staging pieces (frame edges, rows past the bottom) come from a zeroed device
+//    line, so the conversion needs no per-value selects;
+//  * output stores are buffer stores with the step in the scalar offset;
+//  * column max by DPP (2 VALU per value), ReLU as one packed integer max on the two bf16 values
+//    (bf16 bit patterns order as signed 16-bit integers for finite values: max(x, 0) = ReLU).
+__device__ __attribute__((aligned(16))) float stem_zero_line[4] = {0.f, 0.f, 0.f, 0.f};
+// c[e] = max(v[e] of lanes l, l + 1, l + 2 of the lane's 16-lane row) for 4 values: 8 VOP2 DPP
+// maxes.  The s_nop 1 gives the 2 wait states a DPP read needs after the VALU write of its source
+// (the asm is opaque to the compiler's hazard recognizer); the second max of each value reads the
+// first's result as its plain operand.
+__device__ __forceinline__ void colmax4(const f32x4& v, f32x4& c) {
+  float c0, c1, c2, c3;
+  asm("s_nop 1\n\t"
+      "v_max_f32_dpp %0, %4, %4 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %1, %5, %5 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %2, %6, %6 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %3, %7, %7 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %0, %4, %0 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %1, %5, %1 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %2, %6, %2 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_max_f32_dpp %3, %7, %3 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+  c = f32x4{c0, c1, c2, c3};
+}
+constexpr int CB_ROWB = 4 * CB_CH * 16;  // bytes per ring row (4 shifted copies)
+
+__global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(const float* __restrict__ fx,
+                                                                         const u16* __restrict__ w,
+                                                                         const float* __restrict__ bias, u16* y,
+                                                                         int H, int W, int Hs, int Ws, int Hq, int Wq) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 2 * 12 * CB_STG * 4];
+  float* const stg0 = (float*)(ring + CB_LDS);  // [buffer 2][row 4][plane 3][CB_STG]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15;
+  const int q = lane >> 4;
+  const int img = blockIdx.x;
+  const int t0 = blockIdx.y * CB_TILES;
+  const int pc0 = 28 * t0 - 2;
+  const int xs0 = 28 * t0 - 8;
+  const float* fimg = fx + (long long)img * 3 * H * W;
+
+  // ---- weights (registers) and BN shift (+ -inf for stem columns outside the map)
+  bf16x8 wf[4][6];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) wf[j][s] = *(const bf16x8*)(w + (j * 16 + r16) * KSTEM + 32 * s + 8 * q);
+  const int k = 14 * wid + r16;
+  const int m = k & 3;
+  const int sx = 14 * (t0 + wid) - 1 + r16;
+  const float cmask = (sx >= 0 && sx < Ws) ? 0.f : -INFINITY;
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = *(const f32x4*)(bias + j * 16 + 4 * q) + cmask;
+  const int xchunk = m * CB_CH + (12 * k + 4 * m) / 16;
+
+  // ---- B-fragment addresses: k-slice s, lane q reads kernel row kh = min((4s + q) / 3, 6), chunk
+  // c = (4s + q) % 3.  kh = k0[s] + d (d = 0 / 1 by lane); at a step whose compile-time slot of
+  // kh = k0[s] is D = (C + k0[s]) & 15, the read is at D * ROWB + va[s] (D < 15) or vb[s] (D = 15:
+  // the d = 1 lanes wrap to slot 0)
+  constexpr int K0[6] = {0, 1, 2, 4, 5, 6};
+  int va[6], vb[6];
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int g = 4 * s + q;
+    const int kh = min(g / 3, 6), c = g - 3 * (g / 3);
+    const int d = kh - K0[s];
+    const int lc = (xchunk + c) * 16;
+    va[s] = d * CB_ROWB + lc;
+    vb[s] = d ? lc : 15 * CB_ROWB + lc;
+  }
+
+  // ---- staging (f32 plane rows by LDS-DMA; pieces outside the frame read the zero line)
+  auto stage_f32 = [&](int r0, int buf) {
+    float* const stg = stg0 + buf * 12 * CB_STG;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int p = wid + CB_TILES * i;
+      const int rr = p / 3, c = p - 3 * (p / 3);
+      const int yy = r0 + rr - 3;
+      const int xp = xs0 + 4 * lane;
+      const bool ok = (unsigned)yy < (unsigned)H && xp >= 0 && xp + 4 <= W;
+      const float* src = ok ? fimg + ((long long)c * H + yy) * W + xp : stem_zero_line;
+      if (lane < CB_STG / 4) dma16(src, stg + (rr * 3 + c) * CB_STG);
+    }
+  };
+  // conversion task of this thread: ring row drow (0..3) of a step's 4 new rows, column pair dg
+  const bool dtask = tid < 4 * CB_GP;
+  const int drow = dtask ? tid / CB_GP : 0, dg = dtask ? tid - (tid / CB_GP) * CB_GP : 0;
+  const int cst = (drow * 3 * CB_STG + 2 * dg + 3) * 4;  // staging byte offset of (row, plane 0, pair)
+  const int cwr = drow * CB_ROWB + 12 * dg;              // ring byte offset of (row, pair) in copy 0
+
+  // ---- prologue: padded rows 0 .. 12 straight from the frame (global loads, bounds-checked)
+  for (int t = tid; t < 13 * CB_GP; t += 64 * CB_TILES) {
+    const int prow = t / CB_GP, g = t % CB_GP;
+    const int yy = prow - 3;
+    float v[6];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int xx = pc0 + 2 * g + h - 3;
+      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const float* src = fimg + (ok ? (long long)yy * W + xx : 0);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float tv = src[(long long)c * H * W];
+        v[3 * h + c] = ok ? tv : 0.f;
+      }
+    }
+    const unsigned d0 = pack_bf2(v[0], v[1]), d1 = pack_bf2(v[2], v[3]), d2 = pack_bf2(v[4], v[5]);
+    unsigned char* slot = ring + (size_t)((prow + 3) & (RING - 1)) * CB_ROWB + 12 * g;
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      unsigned* d = (unsigned*)(slot + mm * (CB_CH * 16 + 4));
+      d[0] = d0;
+      d[1] = d1;
+      d[2] = d2;
+    }
+  }
+  if (Hq > 2) stage_f32(13, 0);  // padded rows 13 .. 16 (step 2's new rows), converted at step 1
+  __syncthreads();
+
+  // ---- output: buffer stores, lane offset fixed, the pooled row in the scalar offset
+  u16* yimg = y + (long long)img * Hq * Wq * 64;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(yimg, (short)0, Hq * Wq * 128, 0x00020000);
+  const int px = 7 * (t0 + wid) + (r16 >> 1);
+  const bool writer = !(r16 & 1) && r16 <= 12 && px < Wq;
+  const int yvo = writer ? (px * 64 + 4 * q) * 2 : 0x40000000;  // non-writers: out of range, dropped
+
+  const float NEG = -INFINITY;
+  // step py (py = 12 i + U): stem rows 2py (a1) and 2py + 1 (a2), pooled with prev (row 2py - 1)
+  auto step = [&](auto U_, int py, const f32x4 (&prev)[4], f32x4 (&a1)[4], f32x4 (&a2)[4]) {
+    constexpr int U = decltype(U_)::value;
+    // top: the previous step's ring writes and staging DMA are complete for every wave
+    vm_wait<4>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (py + 2 < Hq) stage_f32(4 * py + 13, U & 1);  // rows of step py + 2 (buffer read at step py - 1: done)
+    auto stem_row = [&](auto R_, f32x4 (&acc)[4]) {
+      constexpr int R = decltype(R_)::value;
+      constexpr int C = 4 * (U % 4) + 2 * R + 3;  // slot of kernel row 0 = (prow + 3) & 15, prow = 4 py + 2 R
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const int D = (C + K0[s]) & 15;
+        const unsigned char* a = D == 15 ? ring + vb[s] : ring + D * CB_ROWB + va[s];
+        const bf16x8 xf = *(const bf16x8*)a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xf, s ? acc[j] : bv[j], 0, 0, 0);
+      }
+    };
+    stem_row(std::integral_constant<int, 0>{}, a1);
+    // convert the staged rows 4 py + 9 .. + 12 (step py + 1's new rows; staged at step py - 1)
+    // into ring slots (4 py + 12 + drow) & 15 = 4 ((U + 3) % 4) + drow: no wrap
+    if (py >= 1 && py + 1 < Hq && dtask) {
+      const float* st = (const float*)((const unsigned char*)stg0 + ((U + 1) & 1) * 12 * CB_STG * 4 + cst);
+      float v[6];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[3 * h + c] = st[c * CB_STG + h];
+      const unsigned d0 = pack_bf2(v[0], v[1]), d1 = pack_bf2(v[2], v[3]), d2 = pack_bf2(v[4], v[5]);
+      unsigned char* slot = ring + 4 * ((U + 3) % 4) * CB_ROWB + cwr;
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        unsigned* d = (unsigned*)(slot + mm * (CB_CH * 16 + 4));
+        d[0] = d0;
+        d[1] = d1;
+        d[2] = d2;
+      }
+    }
+    stem_row(std::integral_constant<int, 1>{}, a2);
+    // pool: row max (v_max3), column max over lanes r16, r16 + 1, r16 + 2 of the 16-lane row as two
+    // DPP maxes (the compiler's form was two DPP moves + a v_max3; bound_ctrl reads 0 past the row
+    // end: those lanes are not writers), bf16, ReLU on the packed pair
+    asm volatile("" ::: "memory");  // the stores below stay after this step's staging DMA (vm_wait<4> above)
+    unsigned pk4[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 v, c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(fmaxf(prev[j][e], a1[j][e]), a2[j][e]);
+      colmax4(v, c);
+#pragma unroll
+      for (int e2 = 0; e2 < 2; ++e2) {
+        typedef short s16x2 __attribute__((ext_vector_type(2)));
+        const s16x2 p = __builtin_bit_cast(s16x2, pack_bf2(c[2 * e2], c[2 * e2 + 1]));
+        pk4[j][e2] = __builtin_bit_cast(unsigned, __builtin_elementwise_max(p, (s16x2){0, 0}));
+      }
+    }
+    const int so = py * Wq * 128;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_uint2(pk4[j][0], pk4[j][1])), yr, yvo + 32 * j,
+                                            so, 0);
+    }
+  };
+  f32x4 ra[4], rb[4], rc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ra[j] = f32x4{NEG, NEG, NEG, NEG};
+  // 12 steps per iteration (a uniform exit test after each), rows rotating ra -> (rb, rc) -> (ra, rb)
+  // -> (rc, ra)
+#define EOSV_STEM5_STEP(U, P, A, B)                                        \
+  step(std::integral_constant<int, U>{}, py + U, P, A, B);                 \
+  if (py + U + 1 >= Hq) break;
+  for (int py = 0;; py += 12) {
+    EOSV_STEM5_STEP(0, ra, rb, rc)
+    EOSV_STEM5_STEP(1, rc, ra, rb)
+    EOSV_STEM5_STEP(2, rb, rc, ra)
+    EOSV_STEM5_STEP(3, ra, rb, rc)
+    EOSV_STEM5_STEP(4, rc, ra, rb)
+    EOSV_STEM5_STEP(5, rb, rc, ra)
+    EOSV_STEM5_STEP(6, ra, rb, rc)
+    EOSV_STEM5_STEP(7, rc, ra, rb)
+    EOSV_STEM5_STEP(8, rb, rc, ra)
+    EOSV_STEM5_STEP(9, ra, rb, rc)
+    EOSV_STEM5_STEP(10, rc, ra, rb)
+    EOSV_STEM5_STEP(11, rb, rc, ra)
+  }
+#undef EOSV_STEM5_STEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
 // EOSV_F32X3 stem (column-blocked, DIRECT frames): the same fused stem conv + ReLU + maxpool in
 // split-bf16 arithmetic.  Frames are split as x = x_hi + x_lo and the folded weights as
 // w = w_hi + w_lo (each part bf16, round to nearest), and every MFMA k-slice accumulates
@@ -783,6 +1026,11 @@ static int stem_ahead() {
   return v == 1 ? 1 : 2;
 }
 
+static bool stem_v5() {
+  static const bool v = env_switch("EOSV_STEM_V5", 1) != 0;  // 0 = the r04 column-blocked kernel (A/B switch)
+  return v;
+}
+
 static bool stem_cb() {
   static const bool v = env_switch("EOSV_STEM_CB", 1) != 0;  // 0 = full-width workgroups (A/B switch)
   return v;
@@ -806,10 +1054,13 @@ int launch_stem_pool_bf16(const void* pack, int B, int H, int W, const void* w, 
     if (B <= 0) return EOSV_OK;
     const int ncb = (ntiles + CB_TILES - 1) / CB_TILES;
     if (info) {
-      static const int occ = kernel_occupancy((const void*)stem_pool_bf16_cb_kernel<2>, 64 * CB_TILES);
+      static const int occ = kernel_occupancy((const void*)stem_pool_bf16_cb5_kernel, 64 * CB_TILES);
       return record_launch(info, (long long)B * ncb, occ);
     }
-    if (stem_ahead() == 1)
+    if (stem_v5())
+      hipLaunchKernelGGL(stem_pool_bf16_cb5_kernel, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w,
+                         bias, (u16*)y, H, W, Hs, Ws, Hq, Wq);
+    else if (stem_ahead() == 1)
       hipLaunchKernelGGL(stem_pool_bf16_cb_kernel<1>, dim3(B, ncb), dim3(64 * CB_TILES), 0, s, frames, (const u16*)w,
                          bias, (u16*)y, H, W, Hs, Ws, Hq, Wq);
     else

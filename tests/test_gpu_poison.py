@@ -23,3 +23,25 @@ def test_poisoned_forwards_match_plain():
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "poison_check.py"), "resnet50,resnet18",
                         "bf16,f32", "17,64,130"], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0 and "poison_check: 0 failing" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("name,res", [("resnet18", 224), ("resnet50", 224)])
+def test_r05_stem_bitwise_equal_r04(name, res, tmp_path):
+    """The r05 stem (stem_pool_bf16_cb5_kernel: one barrier per step, unrolled ring addressing,
+    zero-line staging, DPP column max, packed ReLU) against the r04 kernel (EOSV_STEM_V5=0,
+    profiling build): every stage map bitwise equal (37 frames of 224x224, child processes since
+    the switches are read once per process)."""
+    if not os.path.exists(LIB):
+        pytest.fail("libeosv_prof.so missing: run __graft_entry__.build()")
+    outs = []
+    for v5 in ("1", "0"):
+        out = str(tmp_path / f"v5_{v5}.pt")
+        env = dict(os.environ, EOSV_LIBRARY=LIB, EOSV_STEM_V5=v5)
+        r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "ws_diff.py"), "save", out, name, "bf16"],
+                           env=env, capture_output=True, text=True, timeout=200)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(out)
+    import torch
+    a, b = torch.load(outs[0]), torch.load(outs[1])
+    for s, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), f"stage {s} differs between the r05 and r04 stems"
