@@ -76,8 +76,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
 
   // piece -> (row, float4 column) of the operand as stored: TA: A rows are k (BM / 4 pieces per
   // row), else A rows are m (GB_K / 4 pieces per row); B likewise (TB: rows are n)
-  f32x4 ra[AS], rb[BS];
-  auto load = [&](int step) {
+  // two register sets: a step's operands are loaded two k-steps ahead (HBM latency under load is
+  // longer than one k-step of MFMAs at one wave per SIMD)
+  f32x4 ra2[2][AS], rb2[2][BS];
+  auto load = [&](int step, int set) {
+    f32x4 (&ra)[AS] = ra2[set];
+    f32x4 (&rb)[BS] = rb2[set];
     const long long kb = k0 + (long long)step * GB_K;
 #pragma unroll
     for (int s = 0; s < AS; ++s) {
@@ -108,7 +112,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int set) {
+    const f32x4 (&ra)[AS] = ra2[set];
+    const f32x4 (&rb)[BS] = rb2[set];
     float* LAp = lds[buf];
     float* LBp = lds[buf] + GB_K * LA;
 #pragma unroll
@@ -149,13 +155,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
 
   const int q = lane >> 4, c = lane & 15;
   if (steps > 0) {
-    load(0);
-    store(0);
+    load(0, 0);
+    store(0, 0);
+    if (steps > 1) load(1, 1);
+    if (steps > 2) load(2, 0);
     __syncthreads();
   }
   for (int step = 0; step < steps; ++step) {
     const int cur = step & 1;
-    if (step + 1 < steps) load(step + 1);
     const float* LAp = lds[cur];
     const float* LBp = lds[cur] + GB_K * LA;
 #pragma unroll
@@ -168,7 +175,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (step + 1 < steps) store(cur ^ 1);
+    // step + 1's operands (in set (step + 1) & 1, loaded at step - 1 or in the prologue) -> the
+    // other LDS buffer; that set then takes step + 3's
+    if (step + 1 < steps) store(cur ^ 1, cur ^ 1);
+    if (step + 3 < steps) load(step + 3, cur ^ 1);
     __syncthreads();
   }
 

@@ -587,8 +587,8 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
                                                                          const u16* __restrict__ w,
                                                                          const float* __restrict__ bias, u16* y,
                                                                          int H, int W, int Hs, int Ws, int Hq, int Wq) {
-  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 2 * 12 * CB_STG * 4];
-  float* const stg0 = (float*)(ring + CB_LDS);  // [buffer 2][row 4][plane 3][CB_STG]
+  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 3 * 12 * CB_STG * 4];
+  float* const stg0 = (float*)(ring + CB_LDS);  // [buffer 3][row 4][plane 3][CB_STG]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -651,33 +651,48 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
   const int cst = (drow * 3 * CB_STG + 2 * dg + 3) * 4;  // staging byte offset of (row, plane 0, pair)
   const int cwr = drow * CB_ROWB + 12 * dg;              // ring byte offset of (row, pair) in copy 0
 
-  // ---- prologue: padded rows 0 .. 12 straight from the frame (global loads, bounds-checked)
-  for (int t = tid; t < 13 * CB_GP; t += 64 * CB_TILES) {
-    const int prow = t / CB_GP, g = t % CB_GP;
-    const int yy = prow - 3;
-    float v[6];
+  // ---- prologue: the staging of the rows steps 0 and 1 convert (padded rows 9 .. 12 -> buffer 1,
+  // 13 .. 16 -> buffer 2), then padded rows 0 .. 8 straight from the frame (global loads,
+  // bounds-checked; all of a thread's loads issued before any conversion), one drain
+  stage_f32(9, 1);
+  stage_f32(13, 2);
+  {
+    constexpr int NPRO = (9 * CB_GP + 64 * CB_TILES - 1) / (64 * CB_TILES);
+    float v[NPRO][6];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int xx = pc0 + 2 * g + h - 3;
-      const bool ok = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-      const float* src = fimg + (ok ? (long long)yy * W + xx : 0);
+    for (int i = 0; i < NPRO; ++i) {
+      const int t = tid + i * 64 * CB_TILES;
+      const int prow = t / CB_GP, g = t % CB_GP;
+      const int yy = prow - 3;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const float tv = src[(long long)c * H * W];
-        v[3 * h + c] = ok ? tv : 0.f;
+      for (int h = 0; h < 2; ++h) {
+        const int xx = pc0 + 2 * g + h - 3;
+        const bool ok = t < 9 * CB_GP && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const float* src = fimg + (ok ? (long long)yy * W + xx : 0);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float tv = src[(long long)c * H * W];
+          v[i][3 * h + c] = ok ? tv : 0.f;
+        }
       }
     }
-    const unsigned d0 = pack_bf2(v[0], v[1]), d1 = pack_bf2(v[2], v[3]), d2 = pack_bf2(v[4], v[5]);
-    unsigned char* slot = ring + (size_t)((prow + 3) & (RING - 1)) * CB_ROWB + 12 * g;
 #pragma unroll
-    for (int mm = 0; mm < 4; ++mm) {
-      unsigned* d = (unsigned*)(slot + mm * (CB_CH * 16 + 4));
-      d[0] = d0;
-      d[1] = d1;
-      d[2] = d2;
+    for (int i = 0; i < NPRO; ++i) {
+      const int t = tid + i * 64 * CB_TILES;
+      if (t >= 9 * CB_GP) break;
+      const int prow = t / CB_GP, g = t % CB_GP;
+      const unsigned d0 = pack_bf2(v[i][0], v[i][1]), d1 = pack_bf2(v[i][2], v[i][3]), d2 = pack_bf2(v[i][4], v[i][5]);
+      unsigned char* slot = ring + (size_t)((prow + 3) & (RING - 1)) * CB_ROWB + 12 * g;
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        unsigned* d = (unsigned*)(slot + mm * (CB_CH * 16 + 4));
+        d[0] = d0;
+        d[1] = d1;
+        d[2] = d2;
+      }
     }
   }
-  if (Hq > 2) stage_f32(13, 0);  // padded rows 13 .. 16 (step 2's new rows), converted at step 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prologue's staging has landed
   __syncthreads();
 
   // ---- output: buffer stores, lane offset fixed, the pooled row in the scalar offset
@@ -691,30 +706,46 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
   // step py (py = 12 i + U): stem rows 2py (a1) and 2py + 1 (a2), pooled with prev (row 2py - 1)
   auto step = [&](auto U_, int py, const f32x4 (&prev)[4], f32x4 (&a1)[4], f32x4 (&a2)[4]) {
     constexpr int U = decltype(U_)::value;
-    // top: the previous step's ring writes and staging DMA are complete for every wave
-    vm_wait<4>();
+    // top: the previous step's ring writes are complete for every wave (lgkmcnt(0) + barrier), and
+    // so is the staging DMA of step py - 2, which this step converts: younger than its 3 pieces are
+    // that step's 4 output stores and step py - 1's 3 pieces + 4 stores (every step issues exactly
+    // these; steps 0 and 1 convert the prologue's staging, drained before the loop)
+    vm_wait<11>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (py + 2 < Hq) stage_f32(4 * py + 13, U & 1);  // rows of step py + 2 (buffer read at step py - 1: done)
-    auto stem_row = [&](auto R_, f32x4 (&acc)[4]) {
+    // rows 4 py + 17 .. + 20 (converted at step py + 2) into buffer py % 3 (read by step py - 1's
+    // conversion: done); past the frame's last rows the pieces read the zero line, so the count of
+    // pieces per step never changes
+    stage_f32(4 * py + 17, U % 3);
+    // B fragments of stem row 2 py + R: all 6 k-slices read up front (the r04 loop read one,
+    // waited for it and ran its 4 MFMAs, so every k-slice exposed an LDS round trip)
+    auto frags = [&](auto R_, bf16x8 (&xf)[6]) {
       constexpr int R = decltype(R_)::value;
       constexpr int C = 4 * (U % 4) + 2 * R + 3;  // slot of kernel row 0 = (prow + 3) & 15, prow = 4 py + 2 R
 #pragma unroll
       for (int s = 0; s < 6; ++s) {
         const int D = (C + K0[s]) & 15;
         const unsigned char* a = D == 15 ? ring + vb[s] : ring + D * CB_ROWB + va[s];
-        const bf16x8 xf = *(const bf16x8*)a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xf, s ? acc[j] : bv[j], 0, 0, 0);
+        xf[s] = *(const bf16x8*)a;
       }
     };
-    stem_row(std::integral_constant<int, 0>{}, a1);
-    // convert the staged rows 4 py + 9 .. + 12 (step py + 1's new rows; staged at step py - 1)
+    auto stem_row = [&](const bf16x8 (&xf)[6], f32x4 (&acc)[4]) {
+#pragma unroll
+      for (int s = 0; s < 6; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], xf[s], s ? acc[j] : bv[j], 0, 0, 0);
+    };
+    bf16x8 x1[6], x2[6];
+    frags(std::integral_constant<int, 0>{}, x1);
+    frags(std::integral_constant<int, 1>{}, x2);
+    stem_row(x1, a1);
+    // convert the staged rows 4 py + 9 .. + 12 (step py + 1's new rows; staged at step py - 2 into
+    // buffer (py - 2) % 3 = (U + 1) % 3, or by the prologue)
     // into ring slots (4 py + 12 + drow) & 15 = 4 ((U + 3) % 4) + drow: no wrap
-    if (py >= 1 && py + 1 < Hq && dtask) {
-      const float* st = (const float*)((const unsigned char*)stg0 + ((U + 1) & 1) * 12 * CB_STG * 4 + cst);
+    if (py + 1 < Hq && dtask) {
+      const float* st = (const float*)((const unsigned char*)stg0 + ((U + 1) % 3) * 12 * CB_STG * 4 + cst);
       float v[6];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -730,11 +761,11 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
         d[2] = d2;
       }
     }
-    stem_row(std::integral_constant<int, 1>{}, a2);
+    stem_row(x2, a2);
     // pool: row max (v_max3), column max over lanes r16, r16 + 1, r16 + 2 of the 16-lane row as two
     // DPP maxes (the compiler's form was two DPP moves + a v_max3; bound_ctrl reads 0 past the row
     // end: those lanes are not writers), bf16, ReLU on the packed pair
-    asm volatile("" ::: "memory");  // the stores below stay after this step's staging DMA (vm_wait<4> above)
+    asm volatile("" ::: "memory");  // the stores below stay after this step's staging DMA (the vm_wait count above)
     unsigned pk4[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
