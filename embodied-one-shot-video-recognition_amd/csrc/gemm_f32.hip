@@ -28,6 +28,9 @@ namespace eosv {
 namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef EOSV_GEMM_AHEAD_DEF
+#define EOSV_GEMM_AHEAD_DEF 1
+#endif
 constexpr int GB_K = 16;    // reduction rows per k-step
 constexpr int GB_PAD = 16;  // floats of LDS row padding
 
@@ -57,7 +60,7 @@ __device__ __forceinline__ f32x4 load4(const float* __restrict__ p, long long ld
   return v;
 }
 
-template <int WM, int WN, bool TA, bool TB>
+template <int WM, int WN, bool TA, bool TB, int AHEAD>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
   constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 64 * WN;
   constexpr int LA = BM + GB_PAD, LB = BN + GB_PAD;
@@ -76,9 +79,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
 
   // piece -> (row, float4 column) of the operand as stored: TA: A rows are k (BM / 4 pieces per
   // row), else A rows are m (GB_K / 4 pieces per row); B likewise (TB: rows are n)
-  // two register sets: a step's operands are loaded two k-steps ahead (HBM latency under load is
-  // longer than one k-step of MFMAs at one wave per SIMD)
-  f32x4 ra2[2][AS], rb2[2][BS];
+  // AHEAD register sets: a step's operands are loaded AHEAD k-steps before it runs.  1 (default):
+  // 2 was 10 % slower over the R50 finetune shapes (tools/bench_gemm.py, r05: 3.54 vs 3.91 ms; its
+  // second register set costs occupancy), with 8 waves per CU of split-K workgroups hiding the latency
+  static_assert(AHEAD == 1 || AHEAD == 2, "prefetch depth");
+  f32x4 ra2[AHEAD][AS], rb2[AHEAD][BS];
   auto load = [&](int step, int set) {
     f32x4 (&ra)[AS] = ra2[set];
     f32x4 (&rb)[BS] = rb2[set];
@@ -157,8 +162,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
   if (steps > 0) {
     load(0, 0);
     store(0, 0);
-    if (steps > 1) load(1, 1);
-    if (steps > 2) load(2, 0);
+    if (steps > 1) load(1, AHEAD - 1);
+    if (AHEAD == 2 && steps > 2) load(2, 0);
     __syncthreads();
   }
   for (int step = 0; step < steps; ++step) {
@@ -175,10 +180,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    // step + 1's operands (in set (step + 1) & 1, loaded at step - 1 or in the prologue) -> the
-    // other LDS buffer; that set then takes step + 3's
-    if (step + 1 < steps) store(cur ^ 1, cur ^ 1);
-    if (step + 3 < steps) load(step + 3, cur ^ 1);
+    // step + 1's operands (loaded AHEAD - 1 steps ago, or in the prologue) -> the other LDS
+    // buffer; their register set then takes step + 1 + AHEAD's
+    const int set = AHEAD == 2 ? (cur ^ 1) : 0;
+    if (step + 1 < steps) store(cur ^ 1, set);
+    if (step + 1 + AHEAD < steps) load(step + 1 + AHEAD, set);
     __syncthreads();
   }
 
@@ -274,9 +280,13 @@ GemmPlan gemm_plan(int m, int n, int k, bool split) {
   const long long tiles = (long long)p.mt * p.nt;
   long long s = 1;
   if (split) {
-    const long long target = 2LL * device_cu_count();
-    s = std::max(1LL, std::min((target + tiles - 1) / tiles, (long long)k / 1024));
-    s = std::min<long long>(s, 256);
+    // enough workgroups for `wpc` waves per CU (latency hiding: a 64-wide tile has 2 waves), at least
+    // `minrows` reduction rows per slice, at most 1024 slices (the slice sum re-reads slices x m x n)
+    static const int wpc = env_switch("EOSV_GEMM_WPC", 8);
+    static const int minrows = env_switch("EOSV_GEMM_MINROWS", 256);
+    const long long target = (long long)wpc * device_cu_count() / (p.wm * p.wn);
+    s = std::max(1LL, std::min((target + tiles - 1) / tiles, (long long)k / minrows));
+    s = std::min<long long>(s, 1024);
   }
   long long kps = (k + s - 1) / s;
   if (s > 1) kps = (kps + GB_K - 1) / GB_K * GB_K;
@@ -306,11 +316,13 @@ int launch_gemm(bool ta, bool tb, int m, int n, int k, float alpha, const float*
   g.partial = p.slices > 1;
   g.c = g.partial ? work : c;
   const dim3 grid((unsigned)(p.mt * p.nt), (unsigned)p.slices), blk(64 * p.wm * p.wn);
-  const int sel = (p.wm * 2 + p.wn) * 4 + (ta ? 2 : 0) + (tb ? 1 : 0);
-#define EOSV_GEMM_CASE(WM, WN, TA, TB)                                                          \
-  case ((WM * 2 + WN) * 4 + (TA ? 2 : 0) + (TB ? 1 : 0)):                                        \
-    hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TA, TB>), grid, blk, 0, s, g);                   \
+  static const int ahead = env_switch("EOSV_GEMM_AHEAD", EOSV_GEMM_AHEAD_DEF) == 1 ? 1 : 2;  // (A/B switch)
+  const int sel = ((p.wm * 2 + p.wn) * 4 + (ta ? 2 : 0) + (tb ? 1 : 0)) * 2 + (ahead - 1);
+#define EOSV_GEMM_CASE1(WM, WN, TA, TB, AH)                                                   \
+  case (((WM * 2 + WN) * 4 + (TA ? 2 : 0) + (TB ? 1 : 0)) * 2 + AH - 1):                     \
+    hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TA, TB, AH>), grid, blk, 0, s, g);           \
     break;
+#define EOSV_GEMM_CASE(WM, WN, TA, TB) EOSV_GEMM_CASE1(WM, WN, TA, TB, 1) EOSV_GEMM_CASE1(WM, WN, TA, TB, 2)
 #define EOSV_GEMM_TILE(WM, WN) \
   EOSV_GEMM_CASE(WM, WN, false, false) EOSV_GEMM_CASE(WM, WN, false, true) EOSV_GEMM_CASE(WM, WN, true, false) \
   EOSV_GEMM_CASE(WM, WN, true, true)
@@ -323,6 +335,7 @@ int launch_gemm(bool ta, bool tb, int m, int n, int k, float alpha, const float*
   }
 #undef EOSV_GEMM_TILE
 #undef EOSV_GEMM_CASE
+#undef EOSV_GEMM_CASE1
   EOSV_LAUNCH_CHECK();
   if (g.partial) {
     const long long mn = (long long)m * n;

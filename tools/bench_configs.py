@@ -166,8 +166,11 @@ def c3_cpu_baseline(tn, gal, plans, gpu_preds):
         equal += int(int(r["pred"][0]) == int(gp))
     t -= t_synth[0]
     n = len(plans)
-    base = {"value": round(n / t, 4), "unit": "episodes/s", "cores": threads, "kind": "port",
-            "value_backbone_frames_per_s": round(n * (16 + 5 * 16 + 40 * 16) / t, 2),
+    # the same unit as the line's value (backbone frames/s); the oracle, as the reference, forwards
+    # 736 frames per episode (the GPU path 96: it gathers the augmented clips' features), so the
+    # like-for-like rate of the two is episodes_per_s, reported beside it
+    base = {"value": round(n * (16 + 5 * 16 + 40 * 16) / t, 2), "unit": "backbone frames/s", "cores": threads,
+            "kind": "port", "episodes_per_s": round(n / t, 4),
             "sample": f"{n} aug_seg_T episodes through oracle/harness_ref.aug_segment_episode (R50 fp32 torch-CPU, "
                       f"the reference's 736 backbone frames per episode, gallery features from the GPU run, "
                       f"frame synthesis excluded ({t_synth[0]:.1f}s of it), like the configs-1/2/4/5 baselines); {t:.1f}s"}
@@ -185,6 +188,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5, help="configs 4 / 5: timed steps of --episodes episodes")
     ap.add_argument("--cpu-episodes", type=int, default=2, help="config 3: oracle episodes for cpu_baseline (0: none)")
     ap.add_argument("--max-frames", type=int, default=0, help="backbone chunk (default: 4096 config 3, 2048 configs 4 / 5)")
+    ap.add_argument("--cpu-sec", type=float, default=10.0,
+                    help="configs 4 / 5: seconds of oracle CPU time for cpu_baseline / cpu_parity (bench.py "
+                         "--cpu-baseline-sec); C4 needs ~6 s per episode on 16 cores")
+    ap.add_argument("--parity-dump", default=None, help="configs 4 / 5: bench.py --parity-dump")
+    ap.add_argument("--secondary", default="", help="configs 4 / 5: bench.py --secondary-dtype")
     args = ap.parse_args()
     args.episodes = args.episodes or {3: 64, 4: 40, 5: 8}[args.config]
     if args.config == 3:
@@ -195,8 +203,9 @@ def main():
                  "--list", os.path.join(REPO, "tests", "golden", "unreal14.list")],
              5: ["--arch", "resnet101", "--n-way", "5", "--k-shot", "5", "--segments", "32", "--res", "256"]}[args.config]
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), *shape, "--dtype", args.dtype,
-           "--episodes-per-step", str(args.episodes), "--steps", str(args.steps), "--secondary-dtype", "",
-           "--cpu-baseline-sec", "10",
+           "--episodes-per-step", str(args.episodes), "--steps", str(args.steps), "--secondary-dtype", args.secondary,
+           *(["--parity-dump", args.parity_dump] if args.parity_dump else []),
+           "--cpu-baseline-sec", str(args.cpu_sec),
            "--max-frames", str(args.max_frames or 2048), "--config-label", f"BASELINE configs[{args.config - 1}]"]
     sys.exit(subprocess.call(cmd))
 
