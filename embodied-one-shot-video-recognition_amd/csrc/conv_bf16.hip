@@ -899,6 +899,9 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  // R18 stage-2 entry (3x3/2 64 -> 128 at 56x56): row strips with the weights in registers (r05)
+  static const int s2rows = env_switch("EOSV_BF16_S2ROWS", 1);  // 0 = the 512x128 implicit GEMM (A/B switch)
+  if (s2rows && conv_s2rows_bf16_ok(a)) return launch_conv_s2rows_bf16(a, s);
   static const int x3rows = env_switch("EOSV_X3_ROWS", 1);  // 0 = f32x3 stage-1 3x3 convs on the tap-shift kernel (A/B switch)
   if (x3rows && conv_rows_x3_ok(a)) return launch_conv_rows_x3(a, s);
   // tap-shift kernel (conv_bf16_ts.hip) for the stride-1 3x3 convs with Cout = 128 (r01g A/B: 5-6 %

@@ -683,6 +683,8 @@ int main(int argc, char** argv) {
   fails += check_bf16(3, 7, 7, 512, 512, 3, 1, 1, false, true, true);
   fails += check_bf16(2, 9, 11, 128, 128, 3, 1, 1, true, false, true);
   fails += check_bf16(7, 56, 56, 64, 128, 3, 2, 1, false, true);
+  fails += check_bf16(300, 56, 56, 64, 128, 3, 2, 1, false, true);   // stride-2 entry row strips: several per workgroup
+  fails += check_bf16(37, 56, 56, 64, 128, 3, 2, 1, false, false);   // ... without ReLU, ragged strip count
   fails += check_bf16(5, 56, 56, 128, 128, 3, 2, 1, false, true, true);  // R50 layer2.0.conv2 (kcm)
   fails += check_bf16(3, 13, 11, 64, 128, 3, 2, 1, false, true);         // ragged stride-2 entry, M tail
   fails += check_bf16(7, 56, 56, 64, 128, 1, 2, 0, false, false);

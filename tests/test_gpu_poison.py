@@ -25,23 +25,27 @@ def test_poisoned_forwards_match_plain():
     assert r.returncode == 0 and "poison_check: 0 failing" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("name,res", [("resnet18", 224), ("resnet50", 224)])
-def test_r05_stem_bitwise_equal_r04(name, res, tmp_path):
-    """The r05 stem (stem_pool_bf16_cb5_kernel: one barrier per step, unrolled ring addressing,
-    zero-line staging, DPP column max, packed ReLU) against the r04 kernel (EOSV_STEM_V5=0,
-    profiling build): every stage map bitwise equal (37 frames of 224x224, child processes since
-    the switches are read once per process)."""
+@pytest.mark.parametrize("switch,name", [("EOSV_STEM_V5", "resnet18"), ("EOSV_STEM_V5", "resnet50"),
+                                         ("EOSV_BF16_S2ROWS", "resnet18")])
+def test_r05_kernels_bitwise_equal_r04(switch, name, tmp_path):
+    """The r05 kernels against the r04 ones they replace (profiling build, the switch at 0 selects
+    the r04 kernel): every stage map bitwise equal (37 frames of 224x224, child processes since the
+    switches are read once per process).  EOSV_STEM_V5: stem_pool_bf16_cb5_kernel (one barrier per
+    step, unrolled ring addressing, zero-line staging, DPP column max, packed ReLU);
+    EOSV_BF16_S2ROWS: conv_s2rows_bf16 (R18 layer2.0.conv1 row strips) against the 512x128 tile."""
     if not os.path.exists(LIB):
         pytest.fail("libeosv_prof.so missing: run __graft_entry__.build()")
     outs = []
-    for v5 in ("1", "0"):
-        out = str(tmp_path / f"v5_{v5}.pt")
-        env = dict(os.environ, EOSV_LIBRARY=LIB, EOSV_STEM_V5=v5)
+    for v in ("1", "0"):
+        out = str(tmp_path / f"{switch}_{v}.pt")
+        env = dict(os.environ, EOSV_LIBRARY=LIB, **{switch: v})
         r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "ws_diff.py"), "save", out, name, "bf16"],
                            env=env, capture_output=True, text=True, timeout=200)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(out)
     import torch
     a, b = torch.load(outs[0]), torch.load(outs[1])
-    for s, (u, v) in enumerate(zip(a, b)):
-        assert torch.equal(u, v), f"stage {s} differs between the r05 and r04 stems"
+    if not all(torch.equal(u, v) for u, v in zip(a, b)):
+        cmp = subprocess.run([sys.executable, os.path.join(REPO, "tools", "ws_diff.py"), "cmp", outs[0], outs[1]],
+                             capture_output=True, text=True, timeout=120).stdout
+        pytest.fail(f"stage maps differ between the r05 and r04 kernels ({switch}):\n{cmp}")
