@@ -152,6 +152,8 @@ int launch_stem_pool_f32(const void* pack, int B, int H, int W, const void* w, c
                          const float* frames = nullptr);  // non-null: DIRECT (pack unused, may be null)
 bool conv_rows_bf16_ok(const ConvArgs& a);  // conv_rows_bf16.hip: stage-1 3x3 64->64 direct conv
 int launch_conv_rows_bf16(const ConvArgs& a, hipStream_t s);
+bool conv_rowsr_bf16_ok(const ConvArgs& a);  // conv_rowsr_bf16.hip: stage-1 3x3 64->64, weights in registers
+int launch_conv_rowsr_bf16(const ConvArgs& a, hipStream_t s);
 bool conv_s2rows_bf16_ok(const ConvArgs& a);  // conv_s2rows_bf16.hip: R18 stage-2 entry 3x3/2 64->128 row strips
 int launch_conv_s2rows_bf16(const ConvArgs& a, hipStream_t s);
 

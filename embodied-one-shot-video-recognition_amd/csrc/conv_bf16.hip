@@ -850,6 +850,10 @@ static int launch_bf16_ws(const ConvArgs& a, hipStream_t s) {
 #define EOSV_BF16_ARING 1
 #endif
 
+#ifndef EOSV_BF16_ROWSR_DEF
+#define EOSV_BF16_ROWSR_DEF 0
+#endif
+
 static int bf16_rows() {
   static int v = env_switch("EOSV_BF16_ROWS", 1);  // 0 = stage-1 3x3 convs on the implicit GEMM (A/B switch)
   return v;
@@ -898,7 +902,12 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
     return EOSV_ERR_UNSUPPORTED;
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
-  if (bf16_rows() && !a.x2 && !a.split && conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  if (bf16_rows() && !a.x2 && !a.split) {
+    // r05: the weights in registers, three strip buffers (conv_rowsr_bf16.hip); 0 = conv_rows_bf16 (A/B switch)
+    static const int rowsr = env_switch("EOSV_BF16_ROWSR", EOSV_BF16_ROWSR_DEF);
+    if (rowsr && conv_rowsr_bf16_ok(a)) return launch_conv_rowsr_bf16(a, s);
+    if (conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
+  }
   // R18 stage-2 entry (3x3/2 64 -> 128 at 56x56): row strips with the weights in registers (r05)
   static const int s2rows = env_switch("EOSV_BF16_S2ROWS", 1);  // 0 = the 512x128 implicit GEMM (A/B switch)
   if (s2rows && conv_s2rows_bf16_ok(a)) return launch_conv_s2rows_bf16(a, s);
