@@ -126,6 +126,8 @@ static float bf2f(unsigned short v) {
 // bf16 conv through launch_conv_bf16 (stage-1 3x3 shapes take the row-strip kernel, Cout >= 128
 // the phased 8-wave kernel); reference in double on the bf16-rounded operands, checked on images
 // `checked` only
+// the launcher check_bf16 goes through: launch_conv_bf16 (its default dispatch), or one kernel directly
+static int (*g_bf16_launch)(const ConvArgs&, hipStream_t) = launch_conv_bf16;
 static int check_bf16(int N, int H, int W, int Cin, int Cout, int k, int stride, int pad, bool res, bool relu,
                       bool kcm = false) {
   const int K = k * k * Cin;
@@ -161,7 +163,8 @@ static int check_bf16(int N, int H, int W, int Cin, int Cout, int k, int stride,
   a.KH = k; a.KW = k; a.KWp = k; a.stride = stride; a.pad = pad; a.K = K; a.relu = relu; a.zero = dz;
   a.xcd = 1;
   a.kcm = kcm;
-  const int rc = launch_conv_bf16(a, 0);
+  a.xs = Cin;  // dense pixels (launch_conv_bf16 sets it itself)
+  const int rc = g_bf16_launch(a, 0);
   hipDeviceSynchronize();
   std::vector<unsigned short> y(r.size());
   hipMemcpy(y.data(), dy, y.size() * 2, hipMemcpyDeviceToHost);
@@ -683,6 +686,15 @@ int main(int argc, char** argv) {
   fails += check_bf16(3, 7, 7, 512, 512, 3, 1, 1, false, true, true);
   fails += check_bf16(2, 9, 11, 128, 128, 3, 1, 1, true, false, true);
   fails += check_bf16(7, 56, 56, 64, 128, 3, 2, 1, false, true);
+  // r05 register-weight row strips (conv_rowsr_bf16.hip) called directly: C 64 at 56x56, C 128 at 28x28
+  g_bf16_launch = launch_conv_rowsr_bf16;
+  fails += check_bf16(300, 56, 56, 64, 64, 3, 1, 1, true, true);
+  fails += check_bf16(37, 56, 56, 64, 64, 3, 1, 1, false, true);
+  fails += check_bf16(3, 56, 56, 64, 64, 3, 1, 1, true, false);
+  fails += check_bf16(300, 28, 28, 128, 128, 3, 1, 1, true, true);
+  fails += check_bf16(41, 28, 28, 128, 128, 3, 1, 1, false, true);
+  fails += check_bf16(2, 28, 28, 128, 128, 3, 1, 1, true, false);
+  g_bf16_launch = launch_conv_bf16;
   fails += check_bf16(300, 56, 56, 64, 128, 3, 2, 1, false, true);   // stride-2 entry row strips: several per workgroup
   fails += check_bf16(37, 56, 56, 64, 128, 3, 2, 1, false, false);   // ... without ReLU, ragged strip count
   fails += check_bf16(5, 56, 56, 128, 128, 3, 2, 1, false, true, true);  // R50 layer2.0.conv2 (kcm)
