@@ -22,8 +22,9 @@
 // slots 0 and W + 1 are the zero pad) x C / 8 16-B chunks, logical chunk c of (r, p) stored at
 // c ^ swz(p, r) (the XOR applied on the DMA source): swz = p & 7 at C 64 (conv_rows_bf16's),
 // (2 p + 8 r) & 15 at C 128 -- both make every B-fragment ds_read_b128 conflict-free for every
-// tile, tap and k-slice (a simulator of the b128 lane groups of MI355X_MICROARCH.md, LDS; the
-// C 64 swizzle at 256-B slots was 2-3-way).  Out-of-frame rows and the pad slots read a zeroed
+// tile, tap and k-slice (tools/lds_sim.py, a simulator of the b128 lane groups of
+// MI355X_MICROARCH.md, LDS; the C 64 swizzle at 256-B slots: 2.4 LDS cycles per group on average,
+// up to 4-way).  Out-of-frame rows and the pad slots read a zeroed
 // 16-B line (a.zero).
 //
 // Per strip k (buffer k % 3): residual loads of strip k; k-slices 0 .. PPW - 1 each issue one DMA

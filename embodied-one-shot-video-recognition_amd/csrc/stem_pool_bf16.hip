@@ -587,7 +587,8 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
                                                                          const u16* __restrict__ w,
                                                                          const float* __restrict__ bias, u16* y,
                                                                          int H, int W, int Hs, int Ws, int Hq, int Wq) {
-  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 3 * 12 * CB_STG * 4];
+  // + 1 KiB: the destination of the two waves' spare staging instruction (zero lines)
+  __shared__ __attribute__((aligned(16))) unsigned char ring[CB_LDS + 3 * 12 * CB_STG * 4 + 1024];
   float* const stg0 = (float*)(ring + CB_LDS);  // [buffer 3][row 4][plane 3][CB_STG]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -631,18 +632,36 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
     vb[s] = d ? lc : 15 * CB_ROWB + lc;
   }
 
-  // ---- staging (f32 plane rows by LDS-DMA; pieces outside the frame read the zero line)
-  auto stage_f32 = [&](int r0, int buf) {
-    float* const stg = stg0 + buf * 12 * CB_STG;
+  // ---- staging (f32 plane rows by LDS-DMA; pieces outside the frame read the zero line).  A step
+  // stages 12 plane rows (staged row p = 3 rr + c: padded row r0 + rr, plane c) of CB_STG = 32 lanes
+  // x 16 B each, so one DMA instruction carries two consecutive rows: lanes 0-31 row 2 e, lanes 32-63
+  // row 2 e + 1 (the lane's LDS slot is the row base + 16 lane).  Wave w issues pairs e = w and
+  // e = w + 4; waves 2 and 3 have no second pair and DMA zero lines into a spare 1 KiB, so every
+  // wave issues two pieces per step (the counted waits below).  Per lane: its two source rows'
+  // pointers at r0 = 0 and the column-window test, fixed for the kernel; a step adds r0 rows.
+  // (r04: 3 pieces per wave, 30 of 64 lanes active, each piece's address rebuilt in scalar code.)
+  const float* zl = stem_zero_line;
+  asm volatile("" : "+v"(zl));  // one copy held in registers (hipcc rematerialised its address per use)
+  const float* sbase[2];
+  int srr[2];
+  bool scol[2];
+  int sdst[2];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int p = wid + CB_TILES * i;
-      const int rr = p / 3, c = p - 3 * (p / 3);
-      const int yy = r0 + rr - 3;
-      const int xp = xs0 + 4 * lane;
-      const bool ok = (unsigned)yy < (unsigned)H && xp >= 0 && xp + 4 <= W;
-      const float* src = ok ? fimg + ((long long)c * H + yy) * W + xp : stem_zero_line;
-      if (lane < CB_STG / 4) dma16(src, stg + (rr * 3 + c) * CB_STG);
+  for (int i = 0; i < 2; ++i) {
+    const int e = wid + 4 * i;  // row pair
+    const int pr = 2 * e + (lane >> 5), rr = pr / 3, c = pr - 3 * (pr / 3);
+    const int xp = xs0 + 4 * (lane & 31);
+    scol[i] = e < 6 && xp >= 0 && xp + 4 <= W;
+    srr[i] = e < 6 ? rr - 3 : -(1 << 20);
+    sbase[i] = fimg + ((long long)c * H + (rr - 3)) * W + xp;
+    sdst[i] = e < 6 ? 2 * e * CB_STG * 4 : 3 * 12 * CB_STG * 4;  // byte offset from stg0 (spare: past buffer 2)
+  }
+  auto stage_f32 = [&](int r0, int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = scol[i] && (unsigned)(r0 + srr[i]) < (unsigned)H;
+      const int boff = sdst[i] < 3 * 12 * CB_STG * 4 ? buf * 12 * CB_STG * 4 : 0;
+      dma16(ok ? sbase[i] + (long long)r0 * W : zl, (unsigned char*)stg0 + sdst[i] + boff);
     }
   };
   // conversion task of this thread: ring row drow (0..3) of a step's 4 new rows, column pair dg
@@ -707,10 +726,10 @@ __global__ __launch_bounds__(64 * CB_TILES, 2) void stem_pool_bf16_cb5_kernel(co
   auto step = [&](auto U_, int py, const f32x4 (&prev)[4], f32x4 (&a1)[4], f32x4 (&a2)[4]) {
     constexpr int U = decltype(U_)::value;
     // top: the previous step's ring writes are complete for every wave (lgkmcnt(0) + barrier), and
-    // so is the staging DMA of step py - 2, which this step converts: younger than its 3 pieces are
-    // that step's 4 output stores and step py - 1's 3 pieces + 4 stores (every step issues exactly
+    // so is the staging DMA of step py - 2, which this step converts: younger than its 2 pieces are
+    // that step's 4 output stores and step py - 1's 2 pieces + 4 stores (every step issues exactly
     // these; steps 0 and 1 convert the prologue's staging, drained before the loop)
-    vm_wait<11>();
+    vm_wait<10>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
