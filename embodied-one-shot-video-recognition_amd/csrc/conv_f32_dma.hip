@@ -473,6 +473,10 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
   }
 
   // ------------------------------------------------------------------------------------ consumer
+  // profiling-only priority A/B (EOSV_CONV_ABL): 2048 = the second half of the consumers (the
+  // arbitration losers, MI355X_MICROARCH.md "Two waves per SIMD") at priority 1; 4096 = every consumer
+  if ((EOSV_ABL(a) & 2048) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (EOSV_ABL(a) & 4096) __builtin_amdgcn_s_setprio(1);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   f32x16 acc[TM][TN];
 #pragma unroll

@@ -15,8 +15,6 @@ echo "== A/B rowsr (bf16 R18)"
 VAR=EOSV_BF16_ROWSR VALS="0 1" DTYPE=bf16 ROUNDS=2 timeout -k 10 600 bash tools/ab_env.sh 2>&1 | tail -22 || exit 1
 echo "== A/B rowsr (bf16 R50)"
 VAR=EOSV_BF16_ROWSR VALS="0 1" DTYPE=bf16 ARCH=resnet50 ROUNDS=1 timeout -k 10 600 bash tools/ab_env.sh 2>&1 | grep -E "ROWSR|layer +[0-9]:" || exit 1
-echo "== f32 WS ablations (64 no epilogue, 32 no MFMA, 128 no staging, 512 dispatch only)"
-VAR=EOSV_CONV_ABL VALS="0 64 32 128 512" DTYPE=f32 ROUNDS=1 timeout -k 10 600 bash tools/ab_env.sh 2>&1 | tail -22 || exit 1
-echo "== bf16 ablations (1 no prefetch DMA, 2 no residual loads, 64 no epilogue stores; rows kernel = layers 1-4)"
-VAR=EOSV_CONV_ABL VALS="0 1 2 64" DTYPE=bf16 ROUNDS=1 timeout -k 10 600 bash tools/ab_env.sh 2>&1 | tail -22 || exit 1
+echo "== f32 WS ablations (64 no epilogue, 32 no MFMA, 128 no staging, 512 dispatch only; 2048 / 4096 consumer priority)"
+VAR=EOSV_CONV_ABL VALS="0 64 32 128 512 2048 4096" DTYPE=f32 ROUNDS=1 timeout -k 10 600 bash tools/ab_env.sh 2>&1 | tail -24 || exit 1
 echo done
