@@ -2,8 +2,9 @@
 // shapes where all of a conv's folded weights fit one CU's register file (reference models.py:19
 // via self.convnet: torchvision BasicBlock / Bottleneck 3x3 convs at 224 x 224 input):
 //  * C = 64, 56 x 56 (layer1 of ResNet-18/50): r05 successor of conv_rows_bf16.hip;
-//  * C = 128, 28 x 28 (layer2's stride-1 3x3s, no fused downsample): replaces the tap-shift tile
-//    (conv_bf16_ts.hip).
+//  * C = 64, 64 x 64 (layer1 at 256 x 256, config 5's R101): replaces the 128x64 implicit GEMM;
+//  * C = 128, 28 x 28 / 32 x 32 (layer2's stride-1 3x3s, no fused downsample): replaces the tap-shift
+//    tile (conv_bf16_ts.hip); their weights are in the chunk-major K order (ConvArgs::kcm).
 // Each matches the kernel it replaces bit for bit: the same K order per output (C 64: taps
 // ascending, 32-channel halves inside; C 128: the tap-shift order, 32-channel slice outer, kernel
 // row, kernel column), the same MFMA per k-slice and the same epilogue arithmetic
@@ -98,14 +99,18 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
   const u16* __restrict__ w = (const u16*)a.w;
   const u16* zero = (const u16*)a.zero;
 
-  // ---- weights: couts 32 cg + 16 j + r16, k-slice ks: K column tap * C + 32 * cslice + 8 q ..
+  // ---- weights: couts 32 cg + 16 j + r16, k-slice ks: channels c0 = 32 cslice + 8 q .. of its tap,
+  // K column tap * C + c0, or in the chunk-major order (a.kcm, C >= 128 in bf16: 64-channel chunks)
+  // ((c0 / 64) * 9 + tap) * 64 + c0 % 64
   bf16x8 wf[2][P::KS];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int ks = 0; ks < P::KS; ++ks)
-      wf[j][ks] = *(const bf16x8*)(w + (long long)(32 * cg + 16 * j + r16) * a.K + P::tap(ks) * C +
-                                   32 * P::cslice(ks) + 8 * q);
+    for (int ks = 0; ks < P::KS; ++ks) {
+      const int c0 = 32 * P::cslice(ks);
+      const int kc = a.kcm ? ((c0 / 64) * 9 + P::tap(ks)) * 64 + c0 % 64 : P::tap(ks) * C + c0;
+      wf[j][ks] = *(const bf16x8*)(w + (long long)(32 * cg + 16 * j + r16) * a.K + kc + 8 * q);
+    }
   f32x4 bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
             v[1] += bf2f((u16)(rv[u][j].x >> 16));
             v[2] += bf2f((u16)(rv[u][j].y & 0xffff));
             v[3] += bf2f((u16)(rv[u][j].y >> 16));
-          } else if (C == 128) {
+          } else if (!(C == 64 && W == 56)) {  // the implicit GEMM tiles' zero residual (conv_rows_bf16: none)
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += 0.f;
           }
@@ -275,13 +280,19 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
 }
 
 // 0: not a rowsr shape, else the channel count of the instance that takes it
+// 0: not a rowsr shape, else 1 + the instance index (<64, 56>, <64, 64>, <128, 28>, <128, 32>)
 static int rowsr_shape(const ConvArgs& a) {
   const int C = a.Cin;
-  const bool shape = (C == 64 && a.W == 56) || (C == 128 && a.W == 28);
-  return shape && a.Cout == C && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.H % R1_TR == 0 &&
-                 a.Ho == a.H && a.Wo == a.W && a.K == 9 * C && !a.x2 && !a.split && !a.kcm && a.xs == C && a.zero &&
+  int inst = 0;
+  if (C == 64 && a.W == 56) inst = 1;
+  if (C == 64 && a.W == 64) inst = 2;
+  if (C == 128 && a.W == 28) inst = 3;
+  if (C == 128 && a.W == 32) inst = 4;
+  const bool kcm_ok = !a.kcm || (C == 128 && a.kcm == 1);  // bf16 kcm: 64-channel chunks
+  return inst && a.Cout == C && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.H % R1_TR == 0 &&
+                 a.Ho == a.H && a.Wo == a.W && a.K == 9 * C && !a.x2 && !a.split && kcm_ok && a.xs == C && a.zero &&
                  a.N > 0
-             ? C
+             ? inst
              : 0;
 }
 
@@ -290,14 +301,15 @@ bool conv_rowsr_bf16_ok(const ConvArgs& a) { return rowsr_shape(a) != 0; }
 int launch_conv_rowsr_bf16(const ConvArgs& a, hipStream_t s) {
   const long long nstrips = (long long)a.N * (a.H / R1_TR);
   if (nstrips > 0x7fffffffLL) return set_error("conv_rowsr: too many strips"), EOSV_ERR_UNSUPPORTED;
-  const int C = rowsr_shape(a);
-  if (!C) return set_error("conv_rowsr: unsupported shape"), EOSV_ERR_UNSUPPORTED;
+  const int inst = rowsr_shape(a);
+  if (!inst) return set_error("conv_rowsr: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   if (a.plan) return record_launch(a.plan, nstrips, 1);  // persistent: one workgroup per CU walks strips
   const unsigned grid = (unsigned)std::min<long long>(nstrips, device_cu_count());
-  if (C == 64)
-    hipLaunchKernelGGL((conv_rowsr_bf16_kernel<64, 56>), dim3(grid), dim3(64 * R1_NW), 0, s, a, (int)nstrips);
-  else
-    hipLaunchKernelGGL((conv_rowsr_bf16_kernel<128, 28>), dim3(grid), dim3(64 * R1_NW), 0, s, a, (int)nstrips);
+  const dim3 g(grid), b(64 * R1_NW);
+  if (inst == 1) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<64, 56>), g, b, 0, s, a, (int)nstrips);
+  if (inst == 2) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<64, 64>), g, b, 0, s, a, (int)nstrips);
+  if (inst == 3) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<128, 28>), g, b, 0, s, a, (int)nstrips);
+  if (inst == 4) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<128, 32>), g, b, 0, s, a, (int)nstrips);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

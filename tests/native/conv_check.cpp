@@ -694,6 +694,11 @@ int main(int argc, char** argv) {
   fails += check_bf16(300, 28, 28, 128, 128, 3, 1, 1, true, true);
   fails += check_bf16(41, 28, 28, 128, 128, 3, 1, 1, false, true);
   fails += check_bf16(2, 28, 28, 128, 128, 3, 1, 1, true, false);
+  fails += check_bf16(40, 28, 28, 128, 128, 3, 1, 1, true, true, true);   // chunk-major K weights
+  fails += check_bf16(45, 64, 64, 64, 64, 3, 1, 1, true, true);
+  fails += check_bf16(7, 64, 64, 64, 64, 3, 1, 1, false, true);
+  fails += check_bf16(33, 32, 32, 128, 128, 3, 1, 1, true, true, true);
+  fails += check_bf16(6, 32, 32, 128, 128, 3, 1, 1, false, true, true);
   g_bf16_launch = launch_conv_bf16;
   fails += check_bf16(300, 56, 56, 64, 128, 3, 2, 1, false, true);   // stride-2 entry row strips: several per workgroup
   fails += check_bf16(37, 56, 56, 64, 128, 3, 2, 1, false, false);   // ... without ReLU, ragged strip count

@@ -1,6 +1,6 @@
 """Per-stage backbone outputs under the current EOSV_* switches (profiling build), saved to a file,
 or compared with an earlier save: locates the first stage where two kernel choices differ.
-usage: python tools/ws_diff.py save out.pt [arch] [dtype] | python tools/ws_diff.py cmp a.pt b.pt"""
+usage: python tools/ws_diff.py save out.pt [arch[:res]] [dtype] | python tools/ws_diff.py cmp a.pt b.pt"""
 import os
 import sys
 
@@ -11,11 +11,12 @@ sys.path.insert(0, os.path.join(REPO, "embodied-one-shot-video-recognition_amd")
 
 if sys.argv[1] == "save":
     from eosv import arch, engine, synth  # noqa: E402
-    name = sys.argv[3] if len(sys.argv) > 3 else "resnet50"
+    name = sys.argv[3] if len(sys.argv) > 3 else "resnet50"  # arch, or arch:res (e.g. resnet101:256)
+    name, res = (name.split(":")[0], int(name.split(":")[1])) if ":" in name else (name, 224)
     dtype = sys.argv[4] if len(sys.argv) > 4 else "bf16"
     sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
-    x = torch.randn(37, 3, 224, 224, generator=torch.Generator().manual_seed(5)).cuda()
-    bb = engine.Backbone(name, dtype, 224, 224, max_frames=37)
+    x = torch.randn(37, 3, res, res, generator=torch.Generator().manual_seed(5)).cuda()
+    bb = engine.Backbone(name, dtype, res, res, max_frames=37)
     bb.load_state_dict(sd)
     outs = [bb.probe(x, s).float().cpu() for s in range(5)]
     torch.save(outs, sys.argv[2])
