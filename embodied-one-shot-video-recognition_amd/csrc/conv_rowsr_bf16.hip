@@ -30,10 +30,13 @@
 //
 // Per strip k (buffer k % 3): residual loads of strip k; k-slices 0 .. PPW - 1 each issue one DMA
 // piece of strip k + 2 (buffer (k + 2) % 3, read last in strip k - 1, before the barrier that ended
-// it); the next k-slice's 7 fragments are read while this one's 14 MFMAs run; before the epilogue
-// each wave waits for everything but strip k + 2's pieces (vmcnt counts loads, stores and LDS-DMA
-// together in issue order, MI355X_MICROARCH.md): its residual and its pieces of strip k + 1;
-// epilogue from registers (8-B stores, left in flight); lgkmcnt(0) + one barrier.
+// it; zero lines past the last strip, so the count never changes); the next k-slice's 7 fragments
+// are read while this one's 14 MFMAs run; before the epilogue each wave waits for everything but
+// strip k + 2's pieces (vmcnt counts loads, stores and LDS-DMA together in issue order,
+// MI355X_MICROARCH.md): its residual and its pieces of strip k + 1; epilogue from registers (8-B
+// stores, left in flight); lgkmcnt(0) + one barrier.  The waits are the s_waitcnt builtin and the
+// residual / ReLU choices compile-time or branch-free, so hipcc's own wait insertion agrees with
+// them (r05 ISA: no vmcnt wait inside the k-loop or between the epilogue's stores).
 #include <hip/hip_bf16.h>
 
 #include "common.h"
@@ -84,7 +87,9 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
 }
 }  // namespace
 
-template <int C, int W>
+// RES: the conv adds a residual map (a compile-time branch: the epilogue stays one basic block, so
+// hipcc's vmcnt tracking follows the counted waits below and adds none of its own)
+template <int C, int W, bool RES>
 __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs a, int nstrips) {
   using P = RowsR<C, W>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[R1_NBUF * P::BUF];
@@ -155,7 +160,7 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
   constexpr int RV = P::TPP;  // residual registers: one pass's tiles
 
   u16* __restrict__ y = (u16*)a.y;
-  const u16* __restrict__ res = (const u16*)a.res;
+  const u16* __restrict__ res = (const u16*)a.res;  // RES only
   const int G = gridDim.x;
   int strip = xcd_tile(blockIdx.x, G, 1);
 #pragma unroll
@@ -168,18 +173,22 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
       for (int i = 0; i < P::PPW; ++i) piece(i, base, sy0, b);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // waits as the builtin (not inline asm), so that hipcc's own vmcnt tracking sees them
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): weights, bias and the first two strips
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  const float rlow = a.relu ? 0.f : -INFINITY;  // ReLU as max(v, rlow): no branch in the epilogue
 
   for (int k = 0; strip < nstrips; ++k, strip += G) {
     const int cur = k % R1_NBUF;
     const int ahead = strip + 2 * G;
-    const bool issue = ahead < nstrips;
     const int abuf = (k + 2) % R1_NBUF;
-    const u16* abase = x;
-    int ay0 = 0;
-    if (issue) strip_src(ahead, abase, ay0);
+    // strip k + 2's pieces; past the last strip every piece reads the zero line into that buffer
+    // (buffer (k - 1) % 3, never read again), so every strip issues exactly PPW pieces
+    const u16* abase;
+    int ay0;
+    strip_src(ahead < nstrips ? ahead : 0, abase, ay0);
+    if (ahead >= nstrips) ay0 = -(1 << 20);
     const unsigned char* Ib = smem + cur * P::BUF;
     const int img = strip / spi;
     const int y0 = (strip - img * spi) * R1_TR;
@@ -189,17 +198,19 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
     for (int ph = 0; ph < P::NPH; ++ph) {
       const int t0 = ph * P::TPP;                                   // this pass's first tile
       const int nt = ph + 1 < P::NPH ? P::TPP : P::WT - t0;         // and its tile count
-      // residual of this pass's pixels, loaded now so the k-loop hides its latency (inline asm: an
-      // ordinary load's use would make hipcc wait vmcnt(0), draining the DMA pieces in flight)
+      // residual of this pass's pixels, loaded now so the k-loop hides its latency.  Plain loads:
+      // hipcc counts them (and the LDS-DMA pieces issued after them) in its vmcnt before the first
+      // use.  (Inline-asm loads, as conv_rows_bf16 has them, hide the asynchronous register write
+      // from the compiler: here it copied the not-yet-loaded values out right after the asm and
+      // reused a load's destination pair as the next address -- a memory fault, r05.)
       uint2 rv[RV][2];
-      if (res) {
+      if constexpr (RES) {
 #pragma unroll
         for (int u = 0; u < RV; ++u)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             if (u >= nt) continue;
-            const u16* src = res + (obase + 16 * (P::WT * pg + t0 + u) + r16) * C + 32 * cg + 16 * j + 4 * q;
-            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(rv[u][j]) : "v"(src) : "memory");
+            rv[u][j] = *(const uint2*)(res + (obase + 16 * (P::WT * pg + t0 + u) + r16) * C + 32 * cg + 16 * j + 4 * q);
           }
       }
       f32x4 acc[2][RV];
@@ -226,7 +237,7 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
       frags(0, 0);
 #pragma unroll
       for (int ks = 0; ks < P::KS; ++ks) {
-        if (ph == 0 && ks < P::PPW && issue) piece(ks, abase, ay0, abuf);
+        if (ph == 0 && ks < P::PPW) piece(ks, abase, ay0, abuf);
         if (ks + 1 < P::KS) frags(ks + 1, (ks + 1) & 1);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -237,10 +248,10 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
       }
       // pass 0: everything but strip k + 2's pieces has landed (this pass's residual and this wave's
       // pieces of strip k + 1, issued a strip earlier); later passes: their residual, the youngest
-      if (ph == 0 && issue)
-        vm_wait<P::PPW>();
+      if (ph == 0)
+        __builtin_amdgcn_s_waitcnt(0x0f70 | (P::PPW & 15) | ((P::PPW >> 4) << 14));  // vmcnt(PPW)
       else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
       __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
       // epilogue from registers, the replaced kernel's arithmetic: + shift, + residual (the tap-shift
       // tile adds its zero-filled residual when there is none: -0 -> +0), ReLU, bf16
@@ -252,18 +263,17 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[j][u][e] + bias[j][e];
-          if (res) {
+            if constexpr (RES) {
             v[0] += bf2f((u16)(rv[u][j].x & 0xffff));
             v[1] += bf2f((u16)(rv[u][j].x >> 16));
             v[2] += bf2f((u16)(rv[u][j].y & 0xffff));
             v[3] += bf2f((u16)(rv[u][j].y >> 16));
-          } else if (!(C == 64 && W == 56)) {  // the implicit GEMM tiles' zero residual (conv_rows_bf16: none)
+          } else if constexpr (!(C == 64 && W == 56)) {  // the implicit GEMM tiles' zero residual (conv_rows_bf16: none)
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += 0.f;
           }
-          if (a.relu)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], rlow);
           const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
           const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
           *(uint2*)(y + (obase + 16 * (P::WT * pg + t0 + u) + r16) * C + 32 * cg + 16 * j + 4 * q) =
@@ -276,7 +286,7 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): every piece has landed before the workgroup ends
 }
 
 // 0: not a rowsr shape, else the channel count of the instance that takes it
@@ -306,10 +316,14 @@ int launch_conv_rowsr_bf16(const ConvArgs& a, hipStream_t s) {
   if (a.plan) return record_launch(a.plan, nstrips, 1);  // persistent: one workgroup per CU walks strips
   const unsigned grid = (unsigned)std::min<long long>(nstrips, device_cu_count());
   const dim3 g(grid), b(64 * R1_NW);
-  if (inst == 1) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<64, 56>), g, b, 0, s, a, (int)nstrips);
-  if (inst == 2) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<64, 64>), g, b, 0, s, a, (int)nstrips);
-  if (inst == 3) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<128, 28>), g, b, 0, s, a, (int)nstrips);
-  if (inst == 4) hipLaunchKernelGGL((conv_rowsr_bf16_kernel<128, 32>), g, b, 0, s, a, (int)nstrips);
+  const bool r = a.res != nullptr;
+  using K = void (*)(ConvArgs, int);
+  K kern = nullptr;
+  if (inst == 1) kern = r ? (K)conv_rowsr_bf16_kernel<64, 56, true> : (K)conv_rowsr_bf16_kernel<64, 56, false>;
+  if (inst == 2) kern = r ? (K)conv_rowsr_bf16_kernel<64, 64, true> : (K)conv_rowsr_bf16_kernel<64, 64, false>;
+  if (inst == 3) kern = r ? (K)conv_rowsr_bf16_kernel<128, 28, true> : (K)conv_rowsr_bf16_kernel<128, 28, false>;
+  if (inst == 4) kern = r ? (K)conv_rowsr_bf16_kernel<128, 32, true> : (K)conv_rowsr_bf16_kernel<128, 32, false>;
+  hipLaunchKernelGGL(kern, g, b, 0, s, a, (int)nstrips);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
