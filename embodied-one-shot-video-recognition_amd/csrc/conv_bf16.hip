@@ -851,7 +851,7 @@ static int launch_bf16_ws(const ConvArgs& a, hipStream_t s) {
 #endif
 
 #ifndef EOSV_BF16_ROWSR_DEF
-#define EOSV_BF16_ROWSR_DEF 0
+#define EOSV_BF16_ROWSR_DEF 2
 #endif
 
 static int bf16_rows() {
@@ -903,9 +903,14 @@ int launch_conv_bf16(const ConvArgs& a0, hipStream_t s) {
   }
   if (stem) return launch_bf16<128, 64, 2, 2, true>(a, s);
   if (bf16_rows() && !a.x2 && !a.split) {
-    // r05: the weights in registers, three strip buffers (conv_rowsr_bf16.hip); 0 = conv_rows_bf16 (A/B switch)
+    // r05: the weights in registers, three strip buffers (conv_rowsr_bf16.hip).  A/B (r05f, ms per
+    // ~3122-frame launch): C 64 at 64x64 (R101 at 256: the 128x64 implicit GEMM before) 1.57-1.63
+    // -> 0.92-0.98; C 64 at 56x56 0.69 / 0.85 (residual) -> 0.97 / 1.59 against conv_rows_bf16, C 128
+    // at 28x28 / 32x32 0.71-0.78 -> 1.07-1.27 against the tap-shift tile: one wave per SIMD leaves
+    // the LDS-DMA issue and fragment-read latency exposed.  2 (default): only C 64 at 64x64; 1: every
+    // rowsr shape; 0: none (A/B switch)
     static const int rowsr = env_switch("EOSV_BF16_ROWSR", EOSV_BF16_ROWSR_DEF);
-    if (rowsr && conv_rowsr_bf16_ok(a)) return launch_conv_rowsr_bf16(a, s);
+    if (rowsr && conv_rowsr_bf16_ok(a) && (rowsr == 1 || (a.Cin == 64 && a.W == 64))) return launch_conv_rowsr_bf16(a, s);
     if (conv_rows_bf16_ok(a)) return launch_conv_rows_bf16(a, s);
   }
   // R18 stage-2 entry (3x3/2 64 -> 128 at 56x56): row strips with the weights in registers (r05)
