@@ -359,7 +359,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
   const int nt = bt - mt * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int nk = a.K / BK;
-  if (EOSV_ABL(a) & 512) return;  // profiling-only: dispatch cost alone
 
   if (wid >= NW) {  // ---------------------------------------------------------------- producer
     const int pw = wid - NW;
@@ -434,10 +433,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
         __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(As + (pw * (BM / NP) + RPI * j) * BK), 16, 0, 0);
       }
     };
-    if (EOSV_ABL(a) & 128) {  // profiling-only: no staging (the consumers read stale LDS)
-      for (int kt = -1; kt < nk; ++kt) __builtin_amdgcn_s_barrier();
-      return;
-    }
     auto stage_b = [&](int kt) {
       float* Bs = b_slot(kt);
 #pragma unroll
@@ -473,10 +468,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
   }
 
   // ------------------------------------------------------------------------------------ consumer
-  // profiling-only priority A/B (EOSV_CONV_ABL): 2048 = the second half of the consumers (the
-  // arbitration losers, MI355X_MICROARCH.md "Two waves per SIMD") at priority 1; 4096 = every consumer
-  if ((EOSV_ABL(a) & 2048) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  if (EOSV_ABL(a) & 4096) __builtin_amdgcn_s_setprio(1);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -501,10 +492,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
       for (int i = 0; i < TM; ++i) af[i] = *(const f32x4*)(As + (wm * (BM / WM) + i * 32 + r) * BK + pch);
 #pragma unroll
       for (int j = 0; j < TN; ++j) bf[j] = *(const f32x4*)(Bs + (wn * (BN / WN) + j * 32 + r) * BK + pch);
-      if (EOSV_ABL(a) & 32) {  // profiling-only: no MFMAs
-        asm volatile("" ::"v"(af[0]), "v"(bf[0]));
-        continue;
-      }
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
@@ -518,17 +505,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
     asm volatile("" ::: "memory");
   }
 
-  if (EOSV_ABL(a) & 64) {  // profiling-only: no epilogue (every accumulator kept live)
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) sum += acc[i][j][q];
-    asm volatile("" ::"v"(sum));
-    return;
-  }
   // epilogue (conv_f32_dma_kernel's EPI_LDS one; consumer waves only)
   float* __restrict__ y = (float*)a.y;
   const float* __restrict__ res = (const float*)a.res;
