@@ -481,24 +481,33 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
   const int sw = (r / RPB) & (CPR - 1);
   __builtin_amdgcn_s_barrier();  // stage 0 has landed
   asm volatile("" ::: "memory");
+  // Fragment addressing (r05): the 80-VGPR budget of the OCC 2 / NP 4 tile holds the 64
+  // accumulators, the fragments and almost nothing else.  hipcc turned the slot offsets (kt % 3,
+  // kt & 1) into per-lane induction variables and spilled two of them: two scratch reloads with a
+  // vmcnt(0) wait in every K-step.  Now: one lane offset lg0 (chunk g = 1 flips bit 4 of it:
+  // ((2h + 1) ^ sw) = ((2h) ^ sw) ^ 1), the wave-uniform slot offsets through readfirstlane (opaque:
+  // no induction variables), and the A fragment read per row tile (12 fragment VGPRs live, not 16).
+  // The same MFMAs in the same per-accumulator order: bit-identical.
+  const int lg0 = (r * BK + ((h * (BK / 8)) ^ sw) * 4) * 4;
+  const unsigned char* sbase = (const unsigned char*)smem;
   for (int kt = 0; kt < nk; ++kt) {
-    const float* As = a_slot(kt);
-    const float* Bs = b_slot(kt);
+    const int aoff = __builtin_amdgcn_readfirstlane((kt % 3) * AS * 4 + wm * (BM / WM) * BK * 4);
+    const int boff = __builtin_amdgcn_readfirstlane(3 * AS * 4 + (kt & 1) * BS * 4 + wn * (BN / WN) * BK * 4);
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
-      const int pch = ((h * (BK / 8) + g) ^ sw) * 4;
-      f32x4 af[TM], bf[TN];
+      const int lo = g ? (lg0 ^ 16) : lg0;
+      f32x4 bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *(const f32x4*)(As + (wm * (BM / WM) + i * 32 + r) * BK + pch);
+      for (int j = 0; j < TN; ++j) bf[j] = *(const f32x4*)(sbase + boff + lo + j * 32 * BK * 4);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = *(const f32x4*)(Bs + (wn * (BN / WN) + j * 32 + r) * BK + pch);
+      for (int i = 0; i < TM; ++i) {
+        const f32x4 af = *(const f32x4*)(sbase + aoff + lo + i * 32 * BK * 4);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s4], bf[j][s4], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s4], bf[j][s4], acc[i][j], 0, 0, 0);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
