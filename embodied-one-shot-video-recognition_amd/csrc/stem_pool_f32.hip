@@ -228,8 +228,14 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
     if constexpr (DIRECT)
       if (py0 + 1 < py1) direct_rows(4 * py0 + 9, 4);
   }
-  float* yimg = (float*)y + (long long)img * Hq * Wq * 64;
-  unsigned short* ysp = (unsigned short*)y + (long long)img * Hq * Wq * 128;
+  // Output by buffer stores (r05): the resource (this image's pooled map) and the row / tile part of
+  // the offset are wave-uniform (SGPRs), the lane part one VGPR.  The per-tile 64-bit pointers of the
+  // plain stores were 14 VGPRs, two of them spilled: two scratch reloads per step, each waiting
+  // (vmcnt(0)) for the step's stores issued before it.
+  const int obytes = SPLIT ? 256 : 256;  // bytes per pooled pixel: 64 f32, or 128 bf16 (hi, lo)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      (unsigned char*)y + (long long)img * Hq * Wq * obytes, (short)0, Hq * Wq * obytes, 0x00020000);
+  const int yvo = (r16 >> 1) * obytes + (SPLIT ? 2 : 4) * (16 * g + 4 * q);  // lane part
   const bool even = !(r16 & 1);
 
   for (int py = py0; py < py1; ++py) {
@@ -274,6 +280,7 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
         o[e] = fmaxf(c + bv[e], 0.f);
       }
       if (!even || px >= Wq) continue;
+      const int so = (py * Wq + 8 * k) * obytes;  // wave-uniform: pooled row py, tile k
       if constexpr (SPLIT) {
         unsigned hi[2], lo[2];
 #pragma unroll
@@ -286,11 +293,14 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
           lo[h] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(r0)) |
                   ((unsigned)__bfloat16_as_ushort(__float2bfloat16(r1)) << 16);
         }
-        unsigned short* d = ysp + ((long long)py * Wq + px) * 128 + 16 * g + 4 * q;
-        *(uint2*)d = make_uint2(hi[0], hi[1]);
-        *(uint2*)(d + 64) = make_uint2(lo[0], lo[1]);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2){hi[0], hi[1]}, yr, yvo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2){lo[0], lo[1]}, yr, yvo + 128, so, 0);
       } else {
-        *(float4*)(yimg + ((long long)py * Wq + px) * 64 + 16 * g + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
+        typedef float f32x4v __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                                                  (f32x4v){o[0], o[1], o[2], o[3]}),
+                                               yr, yvo, so, 0);
       }
     }
     // every wave's next-step rows have landed (the wait above) and it is done reading the slots
