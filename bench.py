@@ -115,6 +115,8 @@ def cpu_baseline(args, batch, T, emb, preds):
         d = np.sort(cdist(q_emb.astype(np.float64), protos.astype(np.float64))[0])
         margins.append((d[1] - d[0]) / d[0])
         t_load += time.perf_counter() - tc
+        if j % 4 == 3:  # progress on stderr: a long CPU sample must not look hung to a watchdog
+            print(f"cpu_baseline: {j + 1} episodes, {time.perf_counter() - t0 - t_load:.0f}s", file=sys.stderr, flush=True)
         if time.perf_counter() - t0 - t_load > args.cpu_baseline_sec:
             break
     el = time.perf_counter() - t0 - t_load

@@ -164,6 +164,7 @@ def c3_cpu_baseline(tn, gal, plans, gpu_preds):
                                             len(p["support"]) // len(set(p["support_y"])))
         t += time.perf_counter() - t0
         equal += int(int(r["pred"][0]) == int(gp))
+        print(f"c3 cpu_baseline: {equal} of the episodes so far equal, {t:.0f}s", file=sys.stderr, flush=True)
     t -= t_synth[0]
     n = len(plans)
     # the same unit as the line's value (backbone frames/s); the oracle, as the reference, forwards
