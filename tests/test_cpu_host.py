@@ -376,3 +376,22 @@ def test_conv_launch_bytes_and_per_layer_bound():
         floors.append(max(b / hbm * 1e3, fl[i] / (bench.MFMA_PEAK_TF["bf16"] * 1e12) * 1e3))
     assert out["layers"] == int(nl.sum()) and out["hbm_bound_layers"] == int(nl.sum())
     assert abs(out["frac"] - sum(floors) / ms.sum()) < 1e-4
+
+
+def test_row_kernel_lds_layouts_conflict_free():
+    """The LDS images of the row kernels (conv_rows_bf16 / conv_rowsr_bf16.hip: C 64 slots of 128 B
+    with chunk c at c ^ (p & 7); C 128 slots of 256 B with c ^ ((2p + 8r) & 15)) serve every
+    B-fragment ds_read_b128 in 4 LDS cycles (one per lane group: conflict-free), for every pixel
+    tile, tap and 32-channel slice, at the four map widths the kernels take (tools/lds_sim.py,
+    the b128 lane groups of MI355X_MICROARCH.md); the C 64 swizzle at 256-B slots does not."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("lds_sim", os.path.join(REPO, "tools", "lds_sim.py"))
+    sim = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sim)
+    c64 = lambda p, c, r: c ^ (p & 7)  # noqa: E731
+    c128 = lambda p, c, r: c ^ ((2 * p + 8 * r) & 15)  # noqa: E731
+    assert sim.sim(56, 64, 128, c64, 7, 2) == (4, 4.0)
+    assert sim.sim(64, 64, 128, c64, 8, 2) == (4, 4.0)
+    assert sim.sim(28, 128, 256, c128, 7, 1) == (4, 4.0)
+    assert sim.sim(32, 128, 256, c128, 8, 1) == (4, 4.0)
+    assert sim.sim(28, 128, 256, c64, 7, 1)[0] > 4
