@@ -322,21 +322,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
 // rings: 3 A slots (the stage's input row, two stages ahead) and 2 B slots (its 3 taps' weights,
 // one ahead), 147 KiB at 512 x 128.  Same stages, taps, MFMA order and epilogue as
 // conv_bf16_ts_kernel: bit-identical outputs.
-// NBS (r05): B (weight) slots.  2 = the r04 ring (B one stage ahead: issued at the start of the
-// stage before, so its L2 latency had one stage of MFMAs to hide in); 3 = B two stages ahead like A
-// (both rings 3 deep: 384 x 128 tiles, 150.5 KiB).  Same stages, taps, MFMA order and epilogue.
-template <int BM, int BN, int WM, int WN, int NP, int NBS = 2>
+template <int BM, int BN, int WM, int WN, int NP>
 __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(ConvArgs a) {
   constexpr int BK = 32, NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int AR = (BM + 2 + 15) / 16 * 16, AP = AR / 16, APW = (AP + NP - 1) / NP;
   constexpr int BP = 3 * BN / 16, BPW = (BP + NP - 1) / NP;
   constexpr int AS = AR * BK, BS = 3 * BN * BK;  // bf16 elements per A / B slot
-  constexpr int SMEM = 3 * AS + NBS * BS;
-  static_assert(NBS == 2 || NBS == 3, "B ring depth");
-  static_assert(SMEM * 2 <= 163840, "LDS budget");
+  constexpr int SMEM = 3 * AS + 2 * BS;
   __shared__ __attribute__((aligned(16))) u16 smem[SMEM];
   auto a_slot = [&](int st) { return smem + (st % 3) * AS; };
-  auto b_slot = [&](int st) { return smem + 3 * AS + (st % NBS) * BS; };
+  auto b_slot = [&](int st) { return smem + 3 * AS + (st & 1) * BS; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -431,55 +426,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(Co
       else
         vm_wait<APW - 1>();
     };
-    if constexpr (NBS == 3) {
-      // B two stages ahead: stage st + 2 (A and B) is issued while the consumers run stage st, and
-      // each wave waits for everything but its own pieces of stage st + 2 (counted per wave: its A
-      // pieces, and its B pieces of a 3x3 or of a downsample stage)
-      int nb_norm = 0, nb_ds = 0;
-#pragma unroll
-      for (int t = 0; t < BPW; ++t) {
-        nb_norm += (pw + NP * t < BP) ? 1 : 0;
-        nb_ds += (pw + NP * t < BP && btap[t] == 1) ? 1 : 0;
-      }
-      const int na = big ? APW : APW - 1;
-      auto wait_but = [&](int n) {  // all but this wave's n youngest vector-memory operations
-        switch (n) {
-#define EOSV_TS_W(N) \
-  case N:            \
-    vm_wait<N>();    \
-    break;
-          EOSV_TS_W(0) EOSV_TS_W(1) EOSV_TS_W(2) EOSV_TS_W(3) EOSV_TS_W(4) EOSV_TS_W(5) EOSV_TS_W(6)
-          EOSV_TS_W(7) EOSV_TS_W(8) EOSV_TS_W(9) EOSV_TS_W(10) EOSV_TS_W(11) EOSV_TS_W(12) EOSV_TS_W(13)
-          EOSV_TS_W(14) EOSV_TS_W(15)
-#undef EOSV_TS_W
-          default:
-            vm_wait<0>();
-        }
-      };
-      static_assert(APW + BPW <= 15, "wait counts");
-      auto pieces = [&](int st) { return st < nst ? na + (st >= nst3 ? nb_ds : nb_norm) : 0; };
-      if (nst > 0) {
-        stage_a(0);
-        stage_b(0);
-      }
-      if (nst > 1) {
-        stage_a(1);
-        stage_b(1);
-      }
-      wait_but(pieces(1));  // stage 0 has landed
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      for (int st = 0; st < nst; ++st) {  // stage st + 2 out; stage st + 1 lands
-        if (st + 2 < nst) {
-          stage_a(st + 2);
-          stage_b(st + 2);
-        }
-        wait_but(pieces(st + 2));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-      return;
-    }
     if (nst > 0) {
       stage_a(0);
       stage_b(0);
@@ -668,18 +614,7 @@ int launch_conv_bf16_ts(const ConvArgs& a, hipStream_t s) {
   else                                                                                                           \
     hipLaunchKernelGGL((conv_bf16_ts_kernel<BM_, BN_, WM_, WN_, false>), dim3((unsigned)nb), dim3(64 * WM_ * WN_), \
                        0, s, a);
-  static const int tsws = env_switch("EOSV_BF16_TS_WS", EOSV_BF16_TS_WS_DEF);  // 1: warp-specialised 512 x 128 tile (A/B switch; r04: R18 layer-2 3x3s 7-10 %, R50 stage-2 3x3s 4-7 % faster); 2: 384 x 128 with B two stages ahead (r05)
-  if (tsws == 2 && !a.split && a.Cout == 128) {
-    constexpr int NT = 64 * (4 * 2 + 4);
-    const long long nb3 = (M + 383) / 384;
-    if (a.plan) {
-      static const int occ = kernel_occupancy((const void*)conv_bf16_ts_ws_kernel<384, 128, 4, 2, 4, 3>, NT);
-      return record_launch(a.plan, nb3, occ);
-    }
-    hipLaunchKernelGGL((conv_bf16_ts_ws_kernel<384, 128, 4, 2, 4, 3>), dim3((unsigned)nb3), dim3(NT), 0, s, a);
-    EOSV_LAUNCH_CHECK();
-    return EOSV_OK;
-  }
+  static const int tsws = env_switch("EOSV_BF16_TS_WS", EOSV_BF16_TS_WS_DEF);  // 1: warp-specialised 512 x 128 tile (A/B switch; r04: R18 layer-2 3x3s 7-10 %, R50 stage-2 3x3s 4-7 % faster)
   if (tsws && !a.split && a.Cout == 128) {
     constexpr int NT = 64 * (4 * 2 + 4);
     if (a.plan) {
