@@ -18,6 +18,10 @@
 
 #include "common.h"
 
+#ifndef EOSV_F32_KCM_DEF
+#define EOSV_F32_KCM_DEF 0  // release default of the f32 K order (tools/build_variant.sh -DEOSV_F32_KCM_DEF=64)
+#endif
+
 namespace eosv {
 
 static thread_local std::string g_err;
@@ -352,7 +356,7 @@ static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::ve
   // C = 128 1.1x, but the release kernels ran 2-4 % slower with C = 32 (profiling-build A/B:
   // 0.3-0.5 %, C = 64 / 128 0.1-0.3 %): these convs are MFMA-bound with the DMA hidden, so
   // tap-major stays the default
-  static const int f32kcm = env_switch("EOSV_F32_KCM", 0);  // f32 channel chunk (32, 64, 128); 0 = tap-major (A/B switch)
+  static const int f32kcm = env_switch("EOSV_F32_KCM", EOSV_F32_KCM_DEF);  // f32 channel chunk (32, 64, 128); 0 = tap-major (A/B switch)
   c.kcmc = bf16 ? 64 : f32kcm;
   c.kcm = !c.stem && c.kcmc > 0 && c.cinp % c.kcmc == 0 && c.kh * c.kw > 1 && c.kwp == c.kw &&
           (bf16 ? c.cinp > 64 : c.cinp >= 128);

@@ -14,5 +14,5 @@ for f in *.hip; do
     $( [ "$f" = stem_pool_bf16.hip ] && echo -fno-honor-nans ) -c $f -o $out/${f%.hip}.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libeosv_$name.so $out/*.o -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libeosv_$name.so $out/*.o
 echo "built libeosv_$name.so"
