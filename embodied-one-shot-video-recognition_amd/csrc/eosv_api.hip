@@ -19,7 +19,7 @@
 #include "common.h"
 
 #ifndef EOSV_F32_KCM_DEF
-#define EOSV_F32_KCM_DEF 0  // release default of the f32 K order (tools/build_variant.sh -DEOSV_F32_KCM_DEF=64)
+#define EOSV_F32_KCM_DEF 64  // release default of the f32 K order: 64-channel chunk-major (r05), 0 = tap-major
 #endif
 
 namespace eosv {
@@ -354,8 +354,11 @@ static bool fold_conv(Conv& c, const Tensors& t, bool bf16, bool has_bn, std::ve
   // and L2 (4 MB) has turned over, so the tap re-reads come from beyond L2.  r04 (PMC, R18 f32):
   // C = 32 cuts the 256x128 tiles' FETCH_SIZE 3.0x and the fused-downsample ones' 5x, C = 64 2x,
   // C = 128 1.1x, but the release kernels ran 2-4 % slower with C = 32 (profiling-build A/B:
-  // 0.3-0.5 %, C = 64 / 128 0.1-0.3 %): these convs are MFMA-bound with the DMA hidden, so
-  // tap-major stays the default
+  // 0.3-0.5 %, C = 64 / 128 0.1-0.3 %): these convs are MFMA-bound with the DMA hidden.  r05
+  // release A/B (profiles/r05l_ab_f32_kcm64.txt, three interleaved rounds): C = 64 costs the R18
+  // f32 line 0.2-0.3 % (2,322-2,325 -> 2,315-2,320 clips/s) and takes its conv traffic from 2.21x to
+  // 1.39x the algorithmic bytes (6.82 -> 4.30 GB per launch): the default since r05, the re-reads
+  // beyond L2 being bytes every other tenant of the HBM pays for too
   static const int f32kcm = env_switch("EOSV_F32_KCM", EOSV_F32_KCM_DEF);  // f32 channel chunk (32, 64, 128); 0 = tap-major (A/B switch)
   c.kcmc = bf16 ? 64 : f32kcm;
   c.kcm = !c.stem && c.kcmc > 0 && c.cinp % c.kcmc == 0 && c.kh * c.kw > 1 && c.kwp == c.kw &&
