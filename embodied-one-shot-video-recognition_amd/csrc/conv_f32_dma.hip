@@ -334,6 +334,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_f32_dma_kernel(ConvArgs a) 
 // EPD (r05 A/B, EOSV_F32_EPD): the epilogue straight from the accumulators, no LDS staging and no
 // barriers: a 32 x 32 accumulator register is 2 rows x 32 consecutive channels, i.e. two whole
 // 128-B lines per wave instruction for the residual load and the store.
+#ifndef EOSV_F32_PRIO_DEF
+#define EOSV_F32_PRIO_DEF 1  // r05 release A/B (profiles/r05m_ab_f32_prio.txt): 1 +0.26 %, 2 +0.17 % over 0
+#endif
 template <int BM, int BN, int WM, int WN, int NP, bool DS, int OCC, bool EPD = false>
 __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4) void conv_f32_ws_kernel(ConvArgs a) {
   constexpr int BK = 16, CPR = BK / 4, RPI = 64 / CPR, RPB = 64 / BK;
@@ -468,6 +471,12 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
   }
 
   // ------------------------------------------------------------------------------------ consumer
+  // EOSV_F32_PRIO (release-variant A/B, tools/build_variant.sh): 1 = every consumer wave at
+  // priority 1 (the producers' DMA issue then yields the SIMD to MFMA issue), 2 = the second half
+  // of the consumers only (MI355X_MICROARCH.md, "Two waves per SIMD", item 4)
+  if constexpr (EOSV_F32_PRIO_DEF == 1) __builtin_amdgcn_s_setprio(1);
+  if constexpr (EOSV_F32_PRIO_DEF == 2)
+    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   f32x16 acc[TM][TN];
 #pragma unroll
