@@ -12,6 +12,7 @@
 // its gather backward, average pool, softmax cross-entropy, SGD with momentum.
 // Layouts: activations NHWC f32 ([P][C] rows, P = N*H*W), conv weights [Cout][KH][KW][Cin].
 
+#include <climits>
 #include <mutex>
 
 #include "common.h"
@@ -20,6 +21,29 @@ namespace eosv {
 namespace {
 
 constexpr int BN_CHUNKS = 1024;  // row chunks of the two-stage per-channel reductions
+#ifndef EOSV_TRAIN_R04_DEF
+#define EOSV_TRAIN_R04_DEF 0  // 1: the r04 passes by default (A/B builds)
+#endif
+// rows per lane loaded ahead in the batch-norm statistics passes (r05; release A/B variants via
+// tools/build_variant.sh): forward / backward statistics and the finalize's chunks; and the
+// minimum rows per lane of a statistics chunk (r04: 4; 16 since r05: a quarter of the partial-sum
+// bytes written and re-read by the finalize on the narrow-P, wide-C layers)
+#ifndef EOSV_BN_UP0
+#define EOSV_BN_UP0 4
+#endif
+#ifndef EOSV_BN_UP1
+#define EOSV_BN_UP1 4
+#endif
+#ifndef EOSV_BN_UF
+#define EOSV_BN_UF 4
+#endif
+#ifndef EOSV_BN_MINROWS
+#define EOSV_BN_MINROWS 16
+#endif
+// EOSV_TRAIN_R04=1 selects the r04 passes (one row per iteration in the batch-norm statistics,
+// scalar im2col / col2im); read per call in the profiling build (A/B and the bitwise test flip it
+// between calls)
+bool train_r05_passes() { return env_switch("EOSV_TRAIN_R04", EOSV_TRAIN_R04_DEF) == 0; }
 
 int grid_for(long long n, int block = 256) {
   const long long g = (n + block - 1) / block;
@@ -75,6 +99,80 @@ __global__ void col2im_kernel(const float* __restrict__ col, int N, int H, int W
   }
 }
 
+// r05: four consecutive col elements per lane and one 16-byte store; the first element's (pixel,
+// tap, channel) comes from divisions, the next three by carrying the counters.  Bitwise the gather
+// of im2col_kernel (the R50 stem's 0.71 GB col at 96 frames ran at ~1.1 TB/s there: 64-bit
+// divisions per element).  I = int when every index fits, else long long.
+template <typename I>
+__global__ __launch_bounds__(256) void im2col4_kernel(const float* __restrict__ x, int H, int W, int C, int KH,
+                                                      int KW, int stride, int pad, int Ho, int Wo, I total,
+                                                      float* __restrict__ col) {
+  const I K = (I)KH * KW * C, quads = (total + 3) / 4;
+  for (I q = (I)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (I)gridDim.x * blockDim.x) {
+    const I i0 = q * 4, p = i0 / K;
+    const int k = (int)(i0 - p * K);
+    int c = k % C, kw = (k / C) % KW, kh = k / C / KW;
+    int ow = (int)(p % Wo), oh = (int)(p / Wo % Ho);
+    I n = p / Wo / Ho;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+      v[j] = (i0 + j < total && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                 ? x[((n * H + ih) * W + iw) * C + c]
+                 : 0.f;
+      if (++c == C) {
+        c = 0;
+        if (++kw == KW) {
+          kw = 0;
+          if (++kh == KH) {
+            kh = 0;
+            if (++ow == Wo) {
+              ow = 0;
+              if (++oh == Ho) oh = 0, ++n;
+            }
+          }
+        }
+      }
+    }
+    if (i0 + 3 < total)
+      *reinterpret_cast<float4*>(col + i0) = make_float4(v[0], v[1], v[2], v[3]);
+    else
+      for (int j = 0; j < 4 && i0 + j < total; ++j) col[i0 + j] = v[j];
+  }
+}
+
+// r05: col2im_kernel over four channels per lane (C % 4 == 0, 16-byte aligned): float4 loads of
+// dcol and one division chain per four outputs; same taps in the same order, so bitwise equal
+template <typename I>
+__global__ __launch_bounds__(256) void col2im4_kernel(const float4* __restrict__ col, int H, int W, int C4, int KH,
+                                                      int KW, int stride, int pad, int Ho, int Wo, I total4,
+                                                      float4* __restrict__ dx) {
+  const I K4 = (I)KH * KW * C4;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (I)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    const I r = i / C4;
+    const int iw = (int)(r % W), ih = (int)(r / W % H);
+    const I n = r / W / H;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int kh = 0; kh < KH; ++kh) {
+      const int th = ih + pad - kh;
+      if (th < 0 || th % stride) continue;
+      const int oh = th / stride;
+      if (oh >= Ho) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int tw = iw + pad - kw;
+        if (tw < 0 || tw % stride) continue;
+        const int ow = tw / stride;
+        if (ow >= Wo) continue;
+        const float4 v = col[((n * Ho + oh) * Wo + ow) * K4 + (I)(kh * KW + kw) * C4 + c4];
+        s.x += v.x, s.y += v.y, s.z += v.z, s.w += v.w;
+      }
+    }
+    dx[i] = s;
+  }
+}
+
 // V consecutive floats (V = 4: one 16-byte access)
 template <int V>
 __device__ inline void ldv(const float* __restrict__ p, long long i, float (&o)[V]) {
@@ -98,8 +196,10 @@ __device__ inline void stv(float* __restrict__ p, long long i, const float (&o)[
 // with g = dy masked by y > 0 when relu (and written to dres when given).  A block is TC lanes of V
 // channels x (256 / TC) row lanes (TC = min(C / V, 256) rounded to a power of two), reduced in
 // LDS, so narrow layers (C = 64) keep every lane busy.  V = 4 when C % 4 == 0 and the operands
-// are 16-byte aligned.
-template <int MODE, int V>
+// are 16-byte aligned.  U rows per lane are loaded before any is summed (r05: U = 4 keeps four
+// 16-byte loads per operand in flight; U = 1 is the r04 loop); each lane still sums its rows in
+// row order, so the partials are bitwise those of U = 1.
+template <int MODE, int V, int U>
 __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restrict__ a, const float* __restrict__ dy,
                                                           const float* __restrict__ y, int relu, long long P, int C,
                                                           int tc, const float* __restrict__ mean,
@@ -115,31 +215,45 @@ __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restric
   for (int j = 0; j < V; ++j) s0[j] = s1[j] = 0.0;
   if (c < C) {
     if (MODE == 0) {
-      for (long long r = r0 + lr; r < r1; r += nr) {
-        float v[V];
-        ldv<V>(a, r * C + c, v);
-        for (int j = 0; j < V; ++j) {
-          s0[j] += (double)v[j];
-          s1[j] += (double)v[j] * (double)v[j];
-        }
+      for (long long r = r0 + lr; r < r1; r += (long long)U * nr) {
+        float v[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (r + (long long)u * nr < r1) ldv<V>(a, (r + (long long)u * nr) * C + c, v[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (r + (long long)u * nr < r1)
+            for (int j = 0; j < V; ++j) {
+              s0[j] += (double)v[u][j];
+              s1[j] += (double)v[u][j] * (double)v[u][j];
+            }
       }
     } else {
       float m[V], is[V];
       ldv<V>(mean, c, m);
       ldv<V>(invstd, c, is);
-      for (long long r = r0 + lr; r < r1; r += nr) {
-        float g[V], yy[V], x[V];
-        ldv<V>(dy, r * C + c, g);
-        ldv<V>(a, r * C + c, x);
-        if (relu) {
-          ldv<V>(y, r * C + c, yy);
-          for (int j = 0; j < V; ++j)
-            if (!(yy[j] > 0.f)) g[j] = 0.f;
+      for (long long r = r0 + lr; r < r1; r += (long long)U * nr) {
+        float g[U][V], yy[U][V], x[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long i = (r + (long long)u * nr) * C + c;
+          if (r + (long long)u * nr < r1) {
+            ldv<V>(dy, i, g[u]);
+            ldv<V>(a, i, x[u]);
+            if (relu) ldv<V>(y, i, yy[u]);
+          }
         }
-        if (dres) stv<V>(dres, r * C + c, g);
-        for (int j = 0; j < V; ++j) {
-          s0[j] += g[j];
-          s1[j] += (double)g[j] * (double)((x[j] - m[j]) * is[j]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (!(r + (long long)u * nr < r1)) continue;
+          if (relu)
+            for (int j = 0; j < V; ++j)
+              if (!(yy[u][j] > 0.f)) g[u][j] = 0.f;
+          if (dres) stv<V>(dres, (r + (long long)u * nr) * C + c, g[u]);
+          for (int j = 0; j < V; ++j) {
+            s0[j] += g[u][j];
+            s1[j] += (double)g[u][j] * (double)((x[u][j] - m[j]) * is[j]);
+          }
         }
       }
     }
@@ -168,17 +282,18 @@ int bn_lanes(int C) {
   return t;
 }
 
-// row chunks of the two-stage reductions: enough blocks to fill the chip, at least 4 rows per lane
+// row chunks of the two-stage reductions: enough blocks to fill the chip, at least EOSV_BN_MINROWS
+// rows per lane
 int bn_chunks(long long P, int C, int V) {
   const int tc = bn_lanes(C / V), nr = 256 / tc, cblocks = (C / V + tc - 1) / tc;
   long long k = (2048 + cblocks - 1) / cblocks;
-  k = std::min<long long>(k, std::max<long long>(1, P / (4LL * nr)));
+  k = std::min<long long>(k, std::max<long long>(1, P / ((long long)EOSV_BN_MINROWS * nr)));
   return (int)std::max<long long>(1, std::min<long long>(k, BN_CHUNKS));
 }
 
 // the second stage: 8 channel lanes x 32 chunk lanes per block (fixed order, deterministic), then
 // MODE 0 the batch statistics and running estimates, MODE 1 dgamma / dbeta and the sums for dx
-template <int MODE>
+template <int MODE, int U>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int chunks, long long P,
                                                           int C, float eps, float momentum, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, float* __restrict__ out0,
@@ -188,9 +303,17 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
   const int c = blockIdx.x * 8 + lc;
   double s0 = 0.0, s1 = 0.0;
   if (c < C)
-    for (int k = lk; k < chunks; k += 32) {
-      s0 += part[(long long)k * 2 * C + c];
-      s1 += part[(long long)k * 2 * C + C + c];
+    for (int k = lk; k < chunks; k += 32 * U) {
+      double p0[U], p1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k + 32 * u < chunks) {
+          p0[u] = part[(long long)(k + 32 * u) * 2 * C + c];
+          p1[u] = part[(long long)(k + 32 * u) * 2 * C + C + c];
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k + 32 * u < chunks) s0 += p0[u], s1 += p1[u];
     }
   red[0][lk][lc] = s0;
   red[1][lk][lc] = s1;
@@ -601,8 +724,17 @@ int eosv_im2col(const float* d_x, int N, int H, int W, int C, int KH, int KW, in
     return set_error("eosv_im2col: bad argument"), EOSV_ERR_ARG;
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   if (Ho <= 0 || Wo <= 0) return set_error("eosv_im2col: empty output"), EOSV_ERR_ARG;
-  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for((long long)N * Ho * Wo * KH * KW * C)), dim3(256), 0,
-                     (hipStream_t)stream, d_x, N, H, W, C, KH, KW, stride, pad, Ho, Wo, d_col);
+  const hipStream_t s = (hipStream_t)stream;
+  const long long total = (long long)N * Ho * Wo * KH * KW * C;
+  if (!train_r05_passes() || !al16(d_col))
+    hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(total)), dim3(256), 0, s, d_x, N, H, W, C, KH, KW, stride, pad,
+                       Ho, Wo, d_col);
+  else if (total < INT_MAX - 4 && (long long)N * H * W * C < INT_MAX)
+    hipLaunchKernelGGL(im2col4_kernel<int>, dim3(grid_for((total + 3) / 4)), dim3(256), 0, s, d_x, H, W, C, KH, KW,
+                       stride, pad, Ho, Wo, (int)total, d_col);
+  else
+    hipLaunchKernelGGL(im2col4_kernel<long long>, dim3(grid_for((total + 3) / 4)), dim3(256), 0, s, d_x, H, W, C, KH,
+                       KW, stride, pad, Ho, Wo, total, d_col);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -613,8 +745,17 @@ int eosv_col2im(const float* d_col, int N, int H, int W, int C, int KH, int KW, 
     return set_error("eosv_col2im: bad argument"), EOSV_ERR_ARG;
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   if (Ho <= 0 || Wo <= 0) return set_error("eosv_col2im: empty output"), EOSV_ERR_ARG;
-  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
-                     d_col, N, H, W, C, KH, KW, stride, pad, Ho, Wo, d_x);
+  const hipStream_t s = (hipStream_t)stream;
+  const long long total4 = (long long)N * H * W * C / 4, colsz = (long long)N * Ho * Wo * KH * KW * C;
+  if (!train_r05_passes() || C % 4 || !al16(d_col) || !al16(d_x))
+    hipLaunchKernelGGL(col2im_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0, s, d_col, N, H, W, C,
+                       KH, KW, stride, pad, Ho, Wo, d_x);
+  else if (colsz < INT_MAX && 4 * total4 < INT_MAX)
+    hipLaunchKernelGGL(col2im4_kernel<int>, dim3(grid_for(total4)), dim3(256), 0, s, (const float4*)d_col, H, W,
+                       C / 4, KH, KW, stride, pad, Ho, Wo, (int)total4, (float4*)d_x);
+  else
+    hipLaunchKernelGGL(col2im4_kernel<long long>, dim3(grid_for(total4)), dim3(256), 0, s, (const float4*)d_col, H,
+                       W, C / 4, KH, KW, stride, pad, Ho, Wo, total4, (float4*)d_x);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
@@ -633,14 +774,14 @@ int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gam
   const int V = C % 4 == 0 && al16(d_x) ? 4 : 1;
   const int tc = bn_lanes(C / V), chunks = bn_chunks(P, C, V);
   const dim3 pg((C / V + tc - 1) / tc, chunks);
-  if (V == 4)
-    hipLaunchKernelGGL((bn_partials_kernel<0, 4>), pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc,
-                       nullptr, nullptr, nullptr, chunks, part);
-  else
-    hipLaunchKernelGGL((bn_partials_kernel<0, 1>), pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc,
-                       nullptr, nullptr, nullptr, chunks, part);
-  hipLaunchKernelGGL((bn_finalize_kernel<0>), dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, eps,
-                     momentum, d_running_mean, d_running_var, d_save_mean, d_save_invstd, nullptr);
+  const bool un = train_r05_passes();
+  auto partials = V == 4 ? (un ? bn_partials_kernel<0, 4, EOSV_BN_UP0> : bn_partials_kernel<0, 4, 1>)
+                         : (un ? bn_partials_kernel<0, 1, EOSV_BN_UP0> : bn_partials_kernel<0, 1, 1>);
+  hipLaunchKernelGGL(partials, pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc, nullptr, nullptr,
+                     nullptr, chunks, part);
+  auto finalize = un ? bn_finalize_kernel<0, EOSV_BN_UF> : bn_finalize_kernel<0, 1>;
+  hipLaunchKernelGGL(finalize, dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, eps, momentum,
+                     d_running_mean, d_running_var, d_save_mean, d_save_invstd, nullptr);
   if (C % 4 == 0 && al16(d_x) && al16(d_y) && al16(d_residual) && al16(d_save_mean) && al16(d_save_invstd) &&
       al16(d_gamma) && al16(d_beta))
     hipLaunchKernelGGL(bn_apply4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)d_x, (long long)P,
@@ -668,14 +809,14 @@ int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const 
                     : 1;
   const int tc = bn_lanes(C / V), chunks = bn_chunks(P, C, V);
   const dim3 pg((C / V + tc - 1) / tc, chunks);
-  if (V == 4)
-    hipLaunchKernelGGL((bn_partials_kernel<1, 4>), pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc,
-                       d_save_mean, d_save_invstd, d_dres, chunks, part);
-  else
-    hipLaunchKernelGGL((bn_partials_kernel<1, 1>), pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc,
-                       d_save_mean, d_save_invstd, d_dres, chunks, part);
-  hipLaunchKernelGGL((bn_finalize_kernel<1>), dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f,
-                     0.f, nullptr, nullptr, d_dgamma, d_dbeta, sums);
+  const bool un = train_r05_passes();
+  auto partials = V == 4 ? (un ? bn_partials_kernel<1, 4, EOSV_BN_UP1> : bn_partials_kernel<1, 4, 1>)
+                         : (un ? bn_partials_kernel<1, 1, EOSV_BN_UP1> : bn_partials_kernel<1, 1, 1>);
+  hipLaunchKernelGGL(partials, pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc, d_save_mean,
+                     d_save_invstd, d_dres, chunks, part);
+  auto finalize = un ? bn_finalize_kernel<1, EOSV_BN_UF> : bn_finalize_kernel<1, 1>;
+  hipLaunchKernelGGL(finalize, dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f, 0.f, nullptr,
+                     nullptr, d_dgamma, d_dbeta, sums);
   if (C % 4 == 0 && al16(d_dy) && al16(d_y) && al16(d_x) && al16(d_dx) && al16(d_gamma) && al16(d_save_mean) &&
       al16(d_save_invstd))
     hipLaunchKernelGGL(bn_dx4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)d_dy,

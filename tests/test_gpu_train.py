@@ -347,15 +347,17 @@ def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
             assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad + sk.permute(0, 3, 1, 2)) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(3, 40, 5, 7), (4, 256, 41, 43)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
-def test_batchnorm_train_forward_backward_vs_torch(relu, res):
+def test_batchnorm_train_forward_backward_vs_torch(relu, res, shape):
     """eosv_bn_train_forward / _backward against nn.BatchNorm2d in train mode (f64 autograd):
-    output, saved statistics, running estimates, dx, dgamma, dbeta, residual gradient."""
+    output, saved statistics, running estimates, dx, dgamma, dbeta, residual gradient.  The
+    second shape (7052 rows) gives every lane several 4-row groups and a ragged tail."""
     from eosv._lib import lib
 
     L = lib()
     torch.manual_seed(2)
-    N, C, H, W = 3, 40, 5, 7
+    N, C, H, W = shape
     P = N * H * W
     x = torch.randn(N, C, H, W, dtype=torch.float64, requires_grad=True) * 2 + 0.5
     x.retain_grad()
@@ -396,6 +398,23 @@ def test_batchnorm_train_forward_backward_vs_torch(relu, res):
     assert rel(dg, bn.weight.grad) < 1e-5 and rel(db, bn.bias.grad) < 1e-5
     if res:
         assert rel(back(dres), r.grad) < 1e-6
+
+
+def test_train_r05_passes_bitwise_equal_r04():
+    """The r05 training passes against the r04 ones (EOSV_TRAIN_R04=1) on R50-shaped and ragged
+    inputs, every output bitwise equal (tools/train_r05_check.py, profiling build, which reads the
+    switch per call): the batch-norm statistics with 4 rows per lane loaded ahead, im2col with
+    16-byte stores, col2im over four channels per lane."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(repo, "embodied-one-shot-video-recognition_amd", "libeosv_prof.so")
+    if not os.path.exists(prof):
+        pytest.fail("libeosv_prof.so missing: run __graft_entry__.build()")
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "train_r05_check.py")],
+                       env=dict(os.environ, EOSV_LIBRARY=prof), capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0 and "0 differing" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("C", [5, 12])  # scalar and float4 kernels
