@@ -55,6 +55,9 @@ def parse():
                     help="split list to sample episodes from (default: the reference's sources/data/test.list)")
     ap.add_argument("--cpu-baseline-sec", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train-leg", action="store_true",
+                    help="skip the training-step leg (tools/bench_train.py's R50 finetune step; N = 1 and only "
+                         "with the CPU baseline, so --no-cpu-baseline -- every profiling script's -- skips it too)")
     ap.add_argument("--layers", action="store_true", help="print per-layer conv timing to stderr")
     ap.add_argument("--config-label", default="BASELINE configs[1]",
                     help="which BASELINE.json config this run measures (tools/bench_configs.py sets it)")
@@ -444,6 +447,12 @@ def main():
             out["secondary" if i == 0 else "secondary_" + leg["dtype"]] = leg
         if args.layers:
             print_layers(prof, args.dtype)
+        if not args.no_train_leg and not args.no_cpu_baseline and world == 1:
+            # the reference's other entry point (network_train.py finetune step), after
+            # the timed region: R50, its batch of 6 clips x 16 frames at 224x224, f32, 1 + 5 steps
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            from bench_train import measure
+            out["training"] = measure(device=local)[0]
         if not args.no_cpu_baseline and world == 1:
             last = batches[-1].batch
             out["cpu_baseline"], out["cpu_parity"] = cpu_baseline(args, last, T, emb, pred[-len(last.episodes):].cpu().numpy())

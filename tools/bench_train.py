@@ -25,6 +25,34 @@ from eosv.train import NativeTrainer  # noqa: E402
 GFLOP_FWD = {"resnet18": 3.6271, "resnet50": 8.1743}  # per 224x224 frame
 
 
+def measure(arch_name="resnet50", batch=6, frames_per_clip=16, res=224, steps=5, warmup=1, device=0):
+    """One NativeTrainer on synthetic frames: warmup steps, then `steps` timed steps (synchronised
+    on both sides).  Returns the JSON dict, plus the state dict, frames and labels for the CPU leg."""
+    sd = synth.synth_state_dict(arch.SPECS[arch_name], 64, 0)
+    tr = NativeTrainer(arch_name, 64, device=device)
+    tr.load_state_dict(sd)
+    g = torch.Generator().manual_seed(0)
+    frames = torch.randn(batch * frames_per_clip, 3, res, res, generator=g).cuda(device)
+    labels = np.arange(batch) % 64
+    for _ in range(warmup):
+        tr.step(frames, labels, frames_per_clip, 1e-4, 1e-3)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss, _ = tr.step(frames, labels, frames_per_clip, 1e-4, 1e-3)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    nf = batch * frames_per_clip
+    flops = 3 * GFLOP_FWD[arch_name] * 1e9 * (res / 224.0) ** 2 * nf
+    out = {"metric": "training clips/s (network_train.py finetune step)", "arch": arch_name, "batch": batch,
+           "frames_per_clip": frames_per_clip, "res": res, "dtype": "f32", "clips_per_s": round(batch / dt, 2),
+           "frames_per_s": round(nf / dt, 1), "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": warmup,
+           "loss": round(loss, 4), "conv_tflops": round(flops / dt / 1e12, 2),
+           "conv_frac_f32_peak": round(flops / dt / 157.3e12, 4),
+           "data": "synthetic frames, random-init weights of the reference architecture"}
+    return out, sd, frames, labels
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--arch", default="resnet50")
@@ -35,28 +63,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-steps", type=int, default=0)
     a = ap.parse_args()
-    sd = synth.synth_state_dict(arch.SPECS[a.arch], 64, 0)
-    tr = NativeTrainer(a.arch, 64, device=0)
-    tr.load_state_dict(sd)
-    g = torch.Generator().manual_seed(0)
-    frames = torch.randn(a.batch * a.frames, 3, a.res, a.res, generator=g).cuda()
-    labels = np.arange(a.batch) % 64
-    for _ in range(a.warmup):
-        tr.step(frames, labels, a.frames, 1e-4, 1e-3)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss, _ = tr.step(frames, labels, a.frames, 1e-4, 1e-3)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / a.steps
-    nf = a.batch * a.frames
-    scale = (a.res / 224.0) ** 2
-    flops = 3 * GFLOP_FWD[a.arch] * 1e9 * scale * nf
-    out = {"metric": "training clips/s (network_train.py finetune step)", "arch": a.arch, "batch": a.batch,
-           "frames_per_clip": a.frames, "res": a.res, "dtype": "f32", "clips_per_s": round(a.batch / dt, 2),
-           "frames_per_s": round(nf / dt, 1), "ms_per_step": round(dt * 1e3, 2), "loss": round(loss, 4),
-           "conv_tflops": round(flops / dt / 1e12, 2), "conv_frac_f32_peak": round(flops / dt / 157.3e12, 4),
-           "data": "synthetic frames, random-init weights of the reference architecture"}
+    out, sd, frames, labels = measure(a.arch, a.batch, a.frames, a.res, a.steps, a.warmup)
     if a.cpu_steps:
         from oracle.resnet_ref import ModelResNetRef
 
