@@ -40,6 +40,9 @@ constexpr int BN_CHUNKS = 1024;  // row chunks of the two-stage per-channel redu
 #ifndef EOSV_BN_MINROWS
 #define EOSV_BN_MINROWS 16
 #endif
+#ifndef EOSV_BN_GIN
+#define EOSV_BN_GIN 1  // backward dx from the written residual gradient (r05; 0 = from dy and the mask / y)
+#endif
 // EOSV_TRAIN_R04=1 selects the r04 passes (one row per iteration in the batch-norm statistics,
 // scalar im2col / col2im); read per call in the profiling build (A/B and the bitwise test flip it
 // between calls)
@@ -192,8 +195,20 @@ __device__ inline void stv(float* __restrict__ p, long long i, const float (&o)[
   }
 }
 
+// V ReLU-mask bytes (1 = the forward's output > 0; V = 4: one 4-byte access) as "keep" flags
+template <int V>
+__device__ inline void ldm(const uint8_t* __restrict__ p, long long i, bool (&o)[V]) {
+  if constexpr (V == 4) {
+    const unsigned w = *reinterpret_cast<const unsigned*>(p + i);
+    for (int j = 0; j < V; ++j) o[j] = (w >> (8 * j)) & 0xffu;
+  } else {
+    for (int j = 0; j < V; ++j) o[j] = p[i + j] != 0;
+  }
+}
+
 // per (row chunk, channel): partial sums in double.  MODE 0: x, x^2.  MODE 1 (backward): g, g*xhat
-// with g = dy masked by y > 0 when relu (and written to dres when given).  A block is TC lanes of V
+// with g = dy masked by y > 0 when relu (from the forward's mask bytes mk when given, r05, else
+// from y; and written to dres when given).  A block is TC lanes of V
 // channels x (256 / TC) row lanes (TC = min(C / V, 256) rounded to a power of two), reduced in
 // LDS, so narrow layers (C = 64) keep every lane busy.  V = 4 when C % 4 == 0 and the operands
 // are 16-byte aligned.  U rows per lane are loaded before any is summed (r05: U = 4 keeps four
@@ -201,8 +216,9 @@ __device__ inline void stv(float* __restrict__ p, long long i, const float (&o)[
 // row order, so the partials are bitwise those of U = 1.
 template <int MODE, int V, int U>
 __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restrict__ a, const float* __restrict__ dy,
-                                                          const float* __restrict__ y, int relu, long long P, int C,
-                                                          int tc, const float* __restrict__ mean,
+                                                          const float* __restrict__ y,
+                                                          const uint8_t* __restrict__ mk, int relu, long long P,
+                                                          int C, int tc, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, float* __restrict__ dres,
                                                           int chunks, double* __restrict__ part) {
   __shared__ double red[2 * V][256];
@@ -233,14 +249,21 @@ __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restric
       ldv<V>(mean, c, m);
       ldv<V>(invstd, c, is);
       for (long long r = r0 + lr; r < r1; r += (long long)U * nr) {
-        float g[U][V], yy[U][V], x[U][V];
+        float g[U][V], x[U][V];
+        bool keep[U][V];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const long long i = (r + (long long)u * nr) * C + c;
           if (r + (long long)u * nr < r1) {
             ldv<V>(dy, i, g[u]);
             ldv<V>(a, i, x[u]);
-            if (relu) ldv<V>(y, i, yy[u]);
+            if (relu && mk) {
+              ldm<V>(mk, i, keep[u]);
+            } else if (relu) {
+              float yy[V];
+              ldv<V>(y, i, yy);
+              for (int j = 0; j < V; ++j) keep[u][j] = yy[j] > 0.f;
+            }
           }
         }
 #pragma unroll
@@ -248,7 +271,7 @@ __global__ __launch_bounds__(256) void bn_partials_kernel(const float* __restric
           if (!(r + (long long)u * nr < r1)) continue;
           if (relu)
             for (int j = 0; j < V; ++j)
-              if (!(yy[u][j] > 0.f)) g[u][j] = 0.f;
+              if (!keep[u][j]) g[u][j] = 0.f;
           if (dres) stv<V>(dres, (r + (long long)u * nr) * C + c, g[u]);
           for (int j = 0; j < V; ++j) {
             s0[j] += g[u][j];
@@ -351,7 +374,7 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float4* __restrict
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         const float4* __restrict__ res, int relu,
-                                                        float4* __restrict__ y) {
+                                                        float4* __restrict__ y, unsigned* __restrict__ mk) {
   const int lanes = min(C4, 256), nr = 256 / lanes;
   const int lc = threadIdx.x % lanes, lr = threadIdx.x / lanes;
   if (lr >= nr) return;
@@ -371,6 +394,9 @@ __global__ __launch_bounds__(256) void bn_apply4_kernel(const float4* __restrict
       }
       if (relu) o.x = fmaxf(o.x, 0.f), o.y = fmaxf(o.y, 0.f), o.z = fmaxf(o.z, 0.f), o.w = fmaxf(o.w, 0.f);
       y[i] = o;
+      if (mk)  // the backward's ReLU mask: 1 byte per element instead of re-reading y (r05)
+        mk[i] = (unsigned)(o.x > 0.f) | (unsigned)(o.y > 0.f) << 8 | (unsigned)(o.z > 0.f) << 16 |
+                (unsigned)(o.w > 0.f) << 24;
     }
   }
 }
@@ -383,7 +409,8 @@ __device__ inline float bn_dx1(float dy, float y, int relu, float x, float m, fl
 }
 
 __global__ __launch_bounds__(256) void bn_dx4_kernel(const float4* __restrict__ dy, const float4* __restrict__ y,
-                                                     int relu, const float4* __restrict__ x, long long P, int C4,
+                                                     const unsigned* __restrict__ mk, int relu,
+                                                     const float4* __restrict__ x, long long P, int C4,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd,
                                                      const double* __restrict__ sums, float4* __restrict__ dx) {
@@ -401,7 +428,14 @@ __global__ __launch_bounds__(256) void bn_dx4_kernel(const float4* __restrict__ 
     for (long long r = (long long)blockIdx.x * nr + lr; r < P; r += (long long)gridDim.x * nr) {
       const long long i = r * C4 + c4;
       const float4 d = dy[i], v = x[i];
-      const float4 yy = relu ? y[i] : make_float4(1.f, 1.f, 1.f, 1.f);
+      float4 yy = make_float4(1.f, 1.f, 1.f, 1.f);  // relu: only y > 0 matters (bn_dx1)
+      if (relu && mk) {
+        const unsigned w = mk[i];
+        yy = make_float4(w & 0xffu ? 1.f : 0.f, w & 0xff00u ? 1.f : 0.f, w & 0xff0000u ? 1.f : 0.f,
+                         w & 0xff000000u ? 1.f : 0.f);
+      } else if (relu) {
+        yy = y[i];
+      }
       float4 o;
       o.x = bn_dx1(d.x, yy.x, relu, v.x, m.x, is.x, g.x, mg[0], mgx[0]);
       o.y = bn_dx1(d.y, yy.y, relu, v.y, m.y, is.y, g.y, mg[1], mgx[1]);
@@ -415,7 +449,7 @@ __global__ __launch_bounds__(256) void bn_dx4_kernel(const float4* __restrict__ 
 __global__ void bn_apply_kernel(const float* __restrict__ x, long long P, int C, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, const float* __restrict__ res, int relu,
-                                float* __restrict__ y) {
+                                float* __restrict__ y, uint8_t* __restrict__ mk) {
   const long long total = P * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -424,11 +458,13 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, long long P, int C,
     if (res) v += res[i];
     if (relu) v = fmaxf(v, 0.f);
     y[i] = v;
+    if (mk) mk[i] = v > 0.f;
   }
 }
 
 // dx = gamma * invstd * (g - sum(g) / P - xhat * sum(g * xhat) / P)
-__global__ void bn_dx_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu,
+__global__ void bn_dx_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                             const uint8_t* __restrict__ mk, int relu,
                              const float* __restrict__ x, long long P, int C, const float* __restrict__ gamma,
                              const float* __restrict__ mean, const float* __restrict__ invstd,
                              const double* __restrict__ sums, float* __restrict__ dx) {
@@ -436,12 +472,14 @@ __global__ void bn_dx_kernel(const float* __restrict__ dy, const float* __restri
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
-    dx[i] = bn_dx1(dy[i], relu ? y[i] : 1.f, relu, x[i], mean[c], invstd[c], gamma[c], (float)(sums[c] / (double)P),
+    const float yv = !relu ? 1.f : mk ? (mk[i] ? 1.f : 0.f) : y[i];
+    dx[i] = bn_dx1(dy[i], yv, relu, x[i], mean[c], invstd[c], gamma[c], (float)(sums[c] / (double)P),
                    (float)(sums[C + c] / (double)P));
   }
 }
 
 bool al16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; }
+bool al4(const void* p) { return ((uintptr_t)p & 3) == 0; }  // nullptr passes
 
 int rows_grid(long long P, int C) {
   const int nr = 256 / std::min(C / 4, 256);
@@ -764,8 +802,8 @@ int64_t eosv_bn_workspace_bytes(int C) { return C > 0 ? (int64_t)(2 * BN_CHUNKS 
 
 int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gamma, const float* d_beta, float eps,
                           float momentum, float* d_running_mean, float* d_running_var, const float* d_residual,
-                          int relu, float* d_y, float* d_save_mean, float* d_save_invstd, void* d_work,
-                          eosv_stream_t stream) {
+                          int relu, float* d_y, uint8_t* d_mask, float* d_save_mean, float* d_save_invstd,
+                          void* d_work, eosv_stream_t stream) {
   if (!d_x || !d_y || !d_gamma || !d_beta || !d_save_mean || !d_save_invstd || !d_work || !pos(P) || C <= 0 ||
       (!d_running_mean) != (!d_running_var) || !(eps > 0.f))
     return set_error("eosv_bn_train_forward: bad argument"), EOSV_ERR_ARG;
@@ -777,33 +815,38 @@ int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gam
   const bool un = train_r05_passes();
   auto partials = V == 4 ? (un ? bn_partials_kernel<0, 4, EOSV_BN_UP0> : bn_partials_kernel<0, 4, 1>)
                          : (un ? bn_partials_kernel<0, 1, EOSV_BN_UP0> : bn_partials_kernel<0, 1, 1>);
-  hipLaunchKernelGGL(partials, pg, dim3(256), 0, s, d_x, nullptr, nullptr, 0, (long long)P, C, tc, nullptr, nullptr,
-                     nullptr, chunks, part);
+  hipLaunchKernelGGL(partials, pg, dim3(256), 0, s, d_x, nullptr, nullptr, nullptr, 0, (long long)P, C, tc, nullptr,
+                     nullptr, nullptr, chunks, part);
   auto finalize = un ? bn_finalize_kernel<0, EOSV_BN_UF> : bn_finalize_kernel<0, 1>;
   hipLaunchKernelGGL(finalize, dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, eps, momentum,
                      d_running_mean, d_running_var, d_save_mean, d_save_invstd, nullptr);
+  uint8_t* mk = relu ? d_mask : nullptr;  // the ReLU mask for the backward (optional)
   if (C % 4 == 0 && al16(d_x) && al16(d_y) && al16(d_residual) && al16(d_save_mean) && al16(d_save_invstd) &&
-      al16(d_gamma) && al16(d_beta))
+      al16(d_gamma) && al16(d_beta) && al4(mk))
     hipLaunchKernelGGL(bn_apply4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)d_x, (long long)P,
                        C / 4, d_save_mean, d_save_invstd, d_gamma, d_beta, (const float4*)d_residual, relu,
-                       (float4*)d_y);
+                       (float4*)d_y, (unsigned*)mk);
   else
     hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_x, (long long)P, C,
-                       d_save_mean, d_save_invstd, d_gamma, d_beta, d_residual, relu, d_y);
+                       d_save_mean, d_save_invstd, d_gamma, d_beta, d_residual, relu, d_y, mk);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }
 
-int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const float* d_x, int64_t P, int C,
+int eosv_bn_train_backward(const float* d_dy, const float* d_y, const uint8_t* d_mask, int relu, const float* d_x,
+                           int64_t P, int C,
                            const float* d_gamma, const float* d_save_mean, const float* d_save_invstd, float* d_dx,
                            float* d_dgamma, float* d_dbeta, float* d_dres, void* d_work, eosv_stream_t stream) {
   if (!d_dy || !d_x || !d_gamma || !d_save_mean || !d_save_invstd || !d_dx || !d_dgamma || !d_dbeta || !d_work ||
-      !pos(P) || C <= 0 || (relu && !d_y))
+      !pos(P) || C <= 0 || (relu && !d_y && !d_mask))
     return set_error("eosv_bn_train_backward: bad argument"), EOSV_ERR_ARG;
+  // the ReLU mask from the forward's bytes when given (r05: 1 byte per element, not y's 4)
+  const uint8_t* mk = relu ? d_mask : nullptr;
+  const float* yv = mk ? nullptr : d_y;
   const hipStream_t s = (hipStream_t)stream;
   double* part = (double*)d_work;
   double* sums = part + (long long)2 * BN_CHUNKS * C;
-  const int V = C % 4 == 0 && al16(d_x) && al16(d_dy) && al16(d_y) && al16(d_dres) && al16(d_save_mean) &&
+  const int V = C % 4 == 0 && al16(d_x) && al16(d_dy) && al16(yv) && al4(mk) && al16(d_dres) && al16(d_save_mean) &&
                         al16(d_save_invstd)
                     ? 4
                     : 1;
@@ -812,18 +855,25 @@ int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const 
   const bool un = train_r05_passes();
   auto partials = V == 4 ? (un ? bn_partials_kernel<1, 4, EOSV_BN_UP1> : bn_partials_kernel<1, 4, 1>)
                          : (un ? bn_partials_kernel<1, 1, EOSV_BN_UP1> : bn_partials_kernel<1, 1, 1>);
-  hipLaunchKernelGGL(partials, pg, dim3(256), 0, s, d_x, d_dy, d_y, relu, (long long)P, C, tc, d_save_mean,
+  hipLaunchKernelGGL(partials, pg, dim3(256), 0, s, d_x, d_dy, yv, mk, relu, (long long)P, C, tc, d_save_mean,
                      d_save_invstd, d_dres, chunks, part);
   auto finalize = un ? bn_finalize_kernel<1, EOSV_BN_UF> : bn_finalize_kernel<1, 1>;
   hipLaunchKernelGGL(finalize, dim3((C + 7) / 8), dim3(256), 0, s, part, chunks, (long long)P, C, 0.f, 0.f, nullptr,
                      nullptr, d_dgamma, d_dbeta, sums);
-  if (C % 4 == 0 && al16(d_dy) && al16(d_y) && al16(d_x) && al16(d_dx) && al16(d_gamma) && al16(d_save_mean) &&
-      al16(d_save_invstd))
-    hipLaunchKernelGGL(bn_dx4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)d_dy,
-                       (const float4*)d_y, relu, (const float4*)d_x, (long long)P, C / 4, d_gamma, d_save_mean,
+  // r05: with the residual gradient written, it is dy already masked: dx reads it alone (4 bytes per
+  // element instead of dy and the mask / y; bn_dx1 then masks nothing, the same values)
+  const bool g_in = EOSV_BN_GIN && un && d_dres;
+  const float* gdy = g_in ? d_dres : d_dy;
+  const float* gy = g_in ? nullptr : yv;
+  const uint8_t* gmk = g_in ? nullptr : mk;
+  const int grelu = g_in ? 0 : relu;
+  if (C % 4 == 0 && al16(gdy) && al16(gy) && al4(gmk) && al16(d_x) && al16(d_dx) && al16(d_gamma) &&
+      al16(d_save_mean) && al16(d_save_invstd))
+    hipLaunchKernelGGL(bn_dx4_kernel, dim3(rows_grid(P, C)), dim3(256), 0, s, (const float4*)gdy, (const float4*)gy,
+                       (const unsigned*)gmk, grelu, (const float4*)d_x, (long long)P, C / 4, d_gamma, d_save_mean,
                        d_save_invstd, sums, (float4*)d_dx);
   else
-    hipLaunchKernelGGL(bn_dx_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, d_dy, d_y, relu, d_x,
+    hipLaunchKernelGGL(bn_dx_kernel, dim3(grid_for((long long)P * C)), dim3(256), 0, s, gdy, gy, gmk, grelu, d_x,
                        (long long)P, C, d_gamma, d_save_mean, d_save_invstd, sums, d_dx);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;

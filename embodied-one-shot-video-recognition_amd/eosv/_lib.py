@@ -110,8 +110,8 @@ def lib():
         "eosv_im2col": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
         "eosv_col2im": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
         "eosv_bn_workspace_bytes": (i64, [i32]),
-        "eosv_bn_train_forward": (i32, [vp, i64, i32, vp, vp, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp]),
-        "eosv_bn_train_backward": (i32, [vp, vp, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "eosv_bn_train_forward": (i32, [vp, i64, i32, vp, vp, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]),
+        "eosv_bn_train_backward": (i32, [vp, vp, vp, i32, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "eosv_maxpool_forward": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
         "eosv_maxpool_backward": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
         "eosv_avgpool_forward": (i32, [vp, i32, i32, i32, vp, vp]),

@@ -14,6 +14,7 @@ weights [Cout][KH][KW][Cin] (the state_dict's [Cout][Cin][KH][KW] permuted at lo
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -110,6 +111,8 @@ class NativeTrainer:
         self.step_count = 0
         self._scratch: Dict[str, torch.Tensor] = {}
         self._col_key = None  # what the "col" scratch holds (_im2col); reset by every step
+        # the BN backward's ReLU mask from 1-byte forward masks (r05) or from y (EOSV_TRAIN_RELU_MASK=0, A/B)
+        self._relu_mask = os.environ.get("EOSV_TRAIN_RELU_MASK", "1") != "0"
         self.work = torch.empty(int(self.L.eosv_bn_workspace_bytes(2048)) // 4 + 4, dtype=torch.float32,
                                 device=self.dev)
 
@@ -274,21 +277,25 @@ class NativeTrainer:
         return dx
 
     def _bn_fwd(self, z, P, b: _BN, relu, res, s):
+        """Returns y and the backward's saved state: mean, 1/std and, with the ReLU, its mask (one
+        byte per element: the backward reads it instead of y, r05)."""
         y = torch.empty_like(z)
         mean = torch.empty(b.c, dtype=torch.float32, device=self.dev)
         invstd = torch.empty_like(mean)
+        mask = torch.empty(z.numel(), dtype=torch.uint8, device=self.dev) if relu and self._relu_mask else None
         check(self.L.eosv_bn_train_forward(_f(z), P, b.c, _f(b.gamma), _f(b.beta), BN_EPS, BN_MOMENTUM, _f(b.rm),
-                                           _f(b.rv), _f(res), int(relu), _f(y), _f(mean), _f(invstd), _f(self.work),
-                                           s), "eosv_bn_train_forward")
+                                           _f(b.rv), _f(res), int(relu), _f(y), _f(mask), _f(mean), _f(invstd),
+                                           _f(self.work), s), "eosv_bn_train_forward")
         b.nbt += 1
-        return y, (mean, invstd)
+        return y, (mean, invstd, mask)
 
     def _bn_bwd(self, dy, y, relu, z, P, b: _BN, stats, s, want_dres=False):
         dz = torch.empty_like(z)
         dres = torch.empty_like(z) if want_dres else None
-        check(self.L.eosv_bn_train_backward(_f(dy), _f(y), int(relu), _f(z), P, b.c, _f(b.gamma), _f(stats[0]),
-                                            _f(stats[1]), _f(dz), _f(b.dgamma), _f(b.dbeta), _f(dres),
-                                            _f(self.work), s), "eosv_bn_train_backward")
+        mask = stats[2] if relu else None  # None without the forward's mask: y is read
+        check(self.L.eosv_bn_train_backward(_f(dy), None if mask is not None else _f(y), _f(mask), int(relu), _f(z),
+                                            P, b.c, _f(b.gamma), _f(stats[0]), _f(stats[1]), _f(dz), _f(b.dgamma),
+                                            _f(b.dbeta), _f(dres), _f(self.work), s), "eosv_bn_train_backward")
         return dz, dres
 
     # ------------------------------------------------------------------ one iteration

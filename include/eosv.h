@@ -219,17 +219,20 @@ int eosv_col2im(const float* d_col, int N, int H, int W, int C, int KH, int KW, 
                 eosv_stream_t stream);
 /* Batch norm in train mode (nn.BatchNorm2d.train(), eps, momentum): batch mean / biased variance
  * normalise, the running estimates take the unbiased variance; y = bn(x) (+ residual) (ReLU).
- * Saves mean and 1/sqrt(var + eps) for the backward.  d_work: eosv_bn_workspace_bytes(C). */
+ * Saves mean and 1/sqrt(var + eps) for the backward.  d_mask (optional, used with relu): one byte
+ * per element, 1 where y > 0, for the backward (r05).  d_work: eosv_bn_workspace_bytes(C). */
 int64_t eosv_bn_workspace_bytes(int C);
 int eosv_bn_train_forward(const float* d_x, int64_t P, int C, const float* d_gamma, const float* d_beta, float eps,
                           float momentum, float* d_running_mean, float* d_running_var, const float* d_residual,
-                          int relu, float* d_y, float* d_save_mean, float* d_save_invstd, void* d_work,
-                          eosv_stream_t stream);
-/* Its backward from dy = dL/dy (masked by y > 0 when relu): dx, dgamma, dbeta; d_dres (optional)
- * receives the masked dy, the gradient of the residual branch. */
-int eosv_bn_train_backward(const float* d_dy, const float* d_y, int relu, const float* d_x, int64_t P, int C,
-                           const float* d_gamma, const float* d_save_mean, const float* d_save_invstd, float* d_dx,
-                           float* d_dgamma, float* d_dbeta, float* d_dres, void* d_work, eosv_stream_t stream);
+                          int relu, float* d_y, uint8_t* d_mask, float* d_save_mean, float* d_save_invstd,
+                          void* d_work, eosv_stream_t stream);
+/* Its backward from dy = dL/dy (masked by y > 0 when relu: from d_mask when given, else from d_y):
+ * dx, dgamma, dbeta; d_dres (optional) receives the masked dy, the gradient of the residual
+ * branch. */
+int eosv_bn_train_backward(const float* d_dy, const float* d_y, const uint8_t* d_mask, int relu, const float* d_x,
+                           int64_t P, int C, const float* d_gamma, const float* d_save_mean,
+                           const float* d_save_invstd, float* d_dx, float* d_dgamma, float* d_dbeta, float* d_dres,
+                           void* d_work, eosv_stream_t stream);
 /* Max pool 3x3 / 2, pad 1 with argmax indices (first maximum in window order, as torch CPU);
  * backward gathers dy into the argmax positions. */
 int eosv_maxpool_forward(const float* d_x, int N, int H, int W, int C, float* d_y, int32_t* d_idx,

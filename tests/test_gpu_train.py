@@ -132,7 +132,7 @@ def test_train_kernels_reject_bad_arguments():
         check(L.eosv_sgemm(0, 0, 2, 2, 2, 1.0, 0, 2, x.data_ptr(), 2, 0.0, x.data_ptr(), 2, None), "eosv_sgemm")
     with pytest.raises(EosvError):
         check(L.eosv_bn_train_forward(x.data_ptr(), 0, 4, x.data_ptr(), x.data_ptr(), 1e-5, 0.1, 0, 0, 0, 1,
-                                      x.data_ptr(), x.data_ptr(), x.data_ptr(), x.data_ptr(), None),
+                                      x.data_ptr(), None, x.data_ptr(), x.data_ptr(), x.data_ptr(), None),
               "eosv_bn_train_forward")
 
 
@@ -347,12 +347,16 @@ def test_native_conv_and_flipped_dgrad_vs_torch(k, stride, cin, cout, H):
             assert rel(gx.view(N, H, H, cin).permute(0, 3, 1, 2), x.grad + sk.permute(0, 3, 1, 2)) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(3, 40, 5, 7), (4, 256, 41, 43)])
+@pytest.mark.parametrize("shape", [(3, 40, 5, 7), (4, 256, 41, 43), (2, 6, 5, 7)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
-def test_batchnorm_train_forward_backward_vs_torch(relu, res, shape):
+@pytest.mark.parametrize("mask,want_dres", [(False, True), (True, True), (True, False)])
+def test_batchnorm_train_forward_backward_vs_torch(relu, res, shape, mask, want_dres):
     """eosv_bn_train_forward / _backward against nn.BatchNorm2d in train mode (f64 autograd):
     output, saved statistics, running estimates, dx, dgamma, dbeta, residual gradient.  The
-    second shape (7052 rows) gives every lane several 4-row groups and a ragged tail."""
+    second shape (7052 rows) gives every lane several 4-row groups and a ragged tail; the third
+    (C = 6) takes the scalar kernels.  mask: the forward writes the ReLU mask bytes (checked equal
+    to y > 0) and the backward reads them with no y at all; want_dres: with the residual gradient
+    written, dx reads it in place of dy and the mask."""
     from eosv._lib import lib
 
     L = lib()
@@ -380,12 +384,17 @@ def test_batchnorm_train_forward_backward_vs_torch(relu, res, shape):
     rm, rv = rm0.float().cuda(), rv0.float().cuda()
     yd, mean, inv = torch.empty_like(xd), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     work = torch.empty(int(L.eosv_bn_workspace_bytes(C)) // 4 + 4, device="cuda")
+    mk = torch.full((P * C,), 7, dtype=torch.uint8, device="cuda") if mask else None
     _call(L.eosv_bn_train_forward, xd.data_ptr(), P, C, g.data_ptr(), b.data_ptr(), 1e-5, 0.1, rm.data_ptr(),
-          rv.data_ptr(), rd.data_ptr() if res else 0, int(relu), yd.data_ptr(), mean.data_ptr(), inv.data_ptr(),
-          work.data_ptr())
-    dx, dg, db, dres = torch.empty_like(xd), torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty_like(xd)
-    _call(L.eosv_bn_train_backward, dyd.data_ptr(), yd.data_ptr(), int(relu), xd.data_ptr(), P, C, g.data_ptr(),
-          mean.data_ptr(), inv.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), dres.data_ptr(),
+          rv.data_ptr(), rd.data_ptr() if res else 0, int(relu), yd.data_ptr(), mk.data_ptr() if mask else None,
+          mean.data_ptr(), inv.data_ptr(), work.data_ptr())
+    if mask and relu:
+        assert torch.equal(mk.view(P, C).bool(), yd > 0) and int(mk.max()) == 1
+    dx, dg, db = torch.empty_like(xd), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    dres = torch.empty_like(xd) if want_dres else None
+    _call(L.eosv_bn_train_backward, dyd.data_ptr(), None if (mask and relu) else yd.data_ptr(),
+          mk.data_ptr() if mask else None, int(relu), xd.data_ptr(), P, C, g.data_ptr(), mean.data_ptr(),
+          inv.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), dres.data_ptr() if want_dres else None,
           work.data_ptr())
 
     def rel(a, bref):
@@ -396,7 +405,7 @@ def test_batchnorm_train_forward_backward_vs_torch(relu, res, shape):
     assert rel(rm, bn.running_mean) < 1e-6 and rel(rv, bn.running_var) < 1e-6
     assert rel(back(dx), x.grad) < 1e-5
     assert rel(dg, bn.weight.grad) < 1e-5 and rel(db, bn.bias.grad) < 1e-5
-    if res:
+    if res and want_dres:
         assert rel(back(dres), r.grad) < 1e-6
 
 

@@ -1,7 +1,8 @@
 """The r05 training passes against the r04 ones they replace (EOSV_TRAIN_R04=1), same inputs, every
 output bitwise equal:
-  * batch-norm statistics with 4 rows per lane loaded ahead (same row chunks): y, saved mean and
-    inverse std, running estimates, dx, dgamma, dbeta, residual gradient;
+  * batch-norm statistics with 4 rows per lane loaded ahead (same row chunks), the backward's ReLU
+    mask from the forward's mask bytes (no y), dx from the residual gradient when it is written:
+    y, saved mean and inverse std, running estimates, dx, dgamma, dbeta, residual gradient;
   * im2col with four elements and one 16-byte store per lane, col2im over four channels per lane.
 Needs the profiling build (EOSV_LIBRARY=libeosv_prof.so), which reads the switch per call.
 usage: python tools/train_r05_check.py  -> prints 'train_r05_check: <n> cases, <k> differing'"""
@@ -18,10 +19,11 @@ from eosv._lib import check, lib, stream_ptr  # noqa: E402
 # (P rows, C channels, relu, residual, dres): R50 layer shapes at 6 clips x 16 frames / 4 (layer1
 # conv1 / conv3, layer4), ragged row counts (tails of the 4-row groups), the scalar V = 1 path (C = 6)
 CASES = [(75265, 64, True, False, False), (75263, 256, True, True, True), (1177, 2048, True, True, True),
-         (4704, 512, False, False, False), (10007, 6, True, True, True), (97, 40, True, False, True)]
+         (4704, 512, False, False, False), (10007, 6, True, True, True), (10007, 6, True, False, False),
+         (97, 40, True, False, True)]
 
 
-def run(L, P, C, relu, res, dres, seed):
+def run(L, P, C, relu, res, dres, seed, mask=False):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = torch.randn(P, C, device="cuda", generator=g) * 2 + 0.5
     r = torch.randn(P, C, device="cuda", generator=g)
@@ -30,14 +32,17 @@ def run(L, P, C, relu, res, dres, seed):
     bet = torch.randn(C, device="cuda", generator=g)
     rm, rv = torch.randn(C, device="cuda", generator=g), torch.rand(C, device="cuda", generator=g) + 0.5
     y, mean, inv = torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    mk = torch.empty(P * C, dtype=torch.uint8, device="cuda") if mask else None
     work = torch.empty(int(L.eosv_bn_workspace_bytes(C)) // 4 + 4, device="cuda")
     s = stream_ptr()
     check(L.eosv_bn_train_forward(x.data_ptr(), P, C, gam.data_ptr(), bet.data_ptr(), 1e-5, 0.1, rm.data_ptr(),
                                   rv.data_ptr(), r.data_ptr() if res else 0, int(relu), y.data_ptr(),
+                                  mk.data_ptr() if mask else None,
                                   mean.data_ptr(), inv.data_ptr(), work.data_ptr(), s), "eosv_bn_train_forward")
     dx, dg, db = torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     dr = torch.empty_like(x) if dres else None
-    check(L.eosv_bn_train_backward(dy.data_ptr(), y.data_ptr(), int(relu), x.data_ptr(), P, C, gam.data_ptr(),
+    ymk = (None, mk.data_ptr()) if mask and relu else (y.data_ptr(), None)
+    check(L.eosv_bn_train_backward(dy.data_ptr(), *ymk, int(relu), x.data_ptr(), P, C, gam.data_ptr(),
                                    mean.data_ptr(), inv.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
                                    dr.data_ptr() if dres else 0, work.data_ptr(), s), "eosv_bn_train_backward")
     torch.cuda.synchronize()
@@ -71,7 +76,8 @@ def main():
         got = {}
         for old in ("1", "0"):
             os.environ["EOSV_TRAIN_R04"] = old
-            got[old] = run(L, P, C, relu, res, dres, 11 + i)
+            # r05 side: the forward's ReLU mask bytes feed the backward (no y)
+            got[old] = run(L, P, C, relu, res, dres, 11 + i, mask=old == "0")
         names = ["y", "mean", "invstd", "running_mean", "running_var", "dx", "dgamma", "dbeta", "dres"]
         diff = [n for n, a, b in zip(names, got["1"], got["0"]) if not torch.equal(a, b)]
         bad += bool(diff)
