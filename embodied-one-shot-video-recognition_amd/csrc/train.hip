@@ -40,6 +40,15 @@ constexpr int BN_CHUNKS = 1024;  // row chunks of the two-stage per-channel redu
 #ifndef EOSV_BN_MINROWS
 #define EOSV_BN_MINROWS 16
 #endif
+// release A/B knobs (profiles/r05x_ab_bn_grids.txt): workgroups the statistics passes aim for, and
+// the grid cap of the elementwise apply / dx passes (r04: 4096; 1024 since r05, +0.9-1.3 % per
+// training step: each lane's per-channel operands serve more rows; 512 and below lose)
+#ifndef EOSV_BN_BLOCKS
+#define EOSV_BN_BLOCKS 2048
+#endif
+#ifndef EOSV_BN_EW_GRID
+#define EOSV_BN_EW_GRID 1024
+#endif
 #ifndef EOSV_BN_GIN
 #define EOSV_BN_GIN 1  // backward dx from the written residual gradient (r05; 0 = from dy and the mask / y)
 #endif
@@ -309,7 +318,7 @@ int bn_lanes(int C) {
 // rows per lane
 int bn_chunks(long long P, int C, int V) {
   const int tc = bn_lanes(C / V), nr = 256 / tc, cblocks = (C / V + tc - 1) / tc;
-  long long k = (2048 + cblocks - 1) / cblocks;
+  long long k = (EOSV_BN_BLOCKS + cblocks - 1) / cblocks;
   k = std::min<long long>(k, std::max<long long>(1, P / ((long long)EOSV_BN_MINROWS * nr)));
   return (int)std::max<long long>(1, std::min<long long>(k, BN_CHUNKS));
 }
@@ -483,7 +492,7 @@ bool al4(const void* p) { return ((uintptr_t)p & 3) == 0; }  // nullptr passes
 
 int rows_grid(long long P, int C) {
   const int nr = 256 / std::min(C / 4, 256);
-  return (int)std::min<long long>((P + nr - 1) / nr, 4096);
+  return (int)std::min<long long>((P + nr - 1) / nr, EOSV_BN_EW_GRID);
 }
 
 // 3x3 / 2, pad 1 (torchvision's maxpool); argmax = first maximum in (kh, kw) order, as torch CPU
