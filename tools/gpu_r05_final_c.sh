@@ -9,7 +9,7 @@ set -o pipefail
 TAG=r05_c2 timeout -k 10 900 bash tools/gpu_traffic.sh f32 bf16 f32x3 2>&1 | tail -4 || exit 1
 TAG=r05_c3 SCRIPT=tools/bench_configs.py ARGS="--config 3 --cpu-episodes 0" timeout -k 10 600 bash tools/gpu_traffic.sh bf16 2>&1 | tail -3 || exit 1
 C4="--arch resnet50 --n-way 14 --k-shot 1 --segments 16 --list tests/golden/unreal14.list --episodes-per-step 40 --max-frames 2048 --config-label 'BASELINE configs[3]'"
-TAG=r05_c4 ARGS="$C4" timeout -k 10 600 bash tools/gpu_traffic.sh bf16 f32 2>&1 | tail -3 || exit 1
+TAG=r05_c4 ARGS="$C4" timeout -k 10 900 bash tools/gpu_traffic.sh bf16 f32 f32x3 2>&1 | tail -4 || exit 1
 C5="--arch resnet101 --n-way 5 --k-shot 5 --segments 32 --res 256 --episodes-per-step 8 --max-frames 2048 --config-label 'BASELINE configs[4]'"
 TAG=r05_c5 ARGS="$C5" timeout -k 10 600 bash tools/gpu_traffic.sh bf16 2>&1 | tail -3 || exit 1
 echo done
