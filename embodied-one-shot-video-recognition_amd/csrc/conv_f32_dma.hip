@@ -599,21 +599,11 @@ __global__ __launch_bounds__(64 * (WM * WN + NP), (OCC * (WM * WN + NP) + 3) / 4
   }
 }
 
-// split-K (training entry only): enough slices to put ~4 workgroups on every CU, each slice at
-// least 16 K-steps, at most 16 (r05 release A/B, profiles/r05y_ab_ksplit.txt: +2 % per training
-// step over r04's 2 / 32 / 8; 1 per CU and 8 per CU with 8-step slices both -4 %)
-#ifndef EOSV_KS_WPC
-#define EOSV_KS_WPC 4  // workgroups per CU the slices aim for (release A/B knobs)
-#endif
-#ifndef EOSV_KS_MIN
-#define EOSV_KS_MIN 16  // K-steps per slice at least
-#endif
-#ifndef EOSV_KS_MAX
-#define EOSV_KS_MAX 16  // slices at most
-#endif
+// split-K (training entry only): enough slices to put ~2 workgroups on every CU, each slice at
+// least 32 K-steps, at most 8
 static int ksplit_count(long long blocks, int ksteps) {
-  const long long want = ((long long)EOSV_KS_WPC * device_cu_count() + blocks - 1) / blocks;
-  return (int)std::max(1LL, std::min({want, (long long)ksteps / EOSV_KS_MIN, (long long)EOSV_KS_MAX}));
+  const long long want = (2LL * device_cu_count() + blocks - 1) / blocks;
+  return (int)std::max(1LL, std::min({want, (long long)ksteps / 32, 8LL}));
 }
 
 // split-K epilogue: y = relu(sum over slices (in order) + bias + residual), float4 over Cout
