@@ -51,12 +51,6 @@ static_assert(TR * RW == NWAVE * 2 * 16, "strip = 7 waves x 2 pixel tiles");
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)v << 16); }
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
 
-// 16-B LDS read whose placement and wait the caller controls (see the k-step loop)
-__device__ __forceinline__ void ds_read16(bf16x8& v, const u16* p) {
-  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u16*)p;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-}
-
 __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
@@ -154,18 +148,18 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     const int img = strip / spi;
     const int y0 = (strip - img * spi) * TR;
     const long long obase = ((long long)img * H + y0) * RW * 64;  // strip's first output pixel
-    // Residual for the epilogue, loaded now so the MFMA phase hides its latency.  Inline-asm
-    // loads: with an LDS-DMA in flight hipcc waits vmcnt(0) before every use of an ordinary
-    // load's result (and here even before issuing one), which would drain the prefetch.
-    uint2 rv[2][4];
+    // Residual for the epilogue, loaded now so the MFMA phase hides its latency.  Plain loads
+    // (r06): hipcc counts them, and the DMA pieces issued before them, in its own vmcnt tracking,
+    // and their first use is behind the epilogue's vmcnt(0) below, so no wait lands in the k-loop.
+    // (Inline-asm loads hide the asynchronous register write from the compiler, which may then
+    // copy or reuse the destination before the data lands: the r05 conv_rowsr_bf16 fault.)
+    uint2 rv[2][4] = {};
     if (res && !(abl & 2)) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const u16* src = res + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q;
-          asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(rv[mi][j]) : "v"(src) : "memory");
-        }
+        for (int j = 0; j < 4; ++j)
+          rv[mi][j] = *(const uint2*)(res + obase + ((2 * wid + mi) * 16 + r16) * 64 + j * 16 + 4 * q);
     }
 
     f32x4 acc[2][4];
@@ -175,9 +169,11 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
       for (int j = 0; j < 4; ++j) acc[mi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // 18 k-steps (9 taps x two 32-deep slices).  Fragments double-buffered in registers: the
-    // next step's 6 ds_reads are issued (inline asm, so hipcc can neither sink them next to
-    // their MFMAs nor wait lgkmcnt(0) per read) ahead of this step's 8 MFMAs, and one
-    // lgkmcnt(0) per step retires them; sched_barrier keeps each step's MFMAs inside it.
+    // next step's 6 ds_reads go out ahead of this step's 8 MFMAs (sched_barrier keeps each step's
+    // reads and MFMAs in place), and one lgkmcnt(0) after them retires the next step's reads.
+    // Plain LDS loads and the s_waitcnt builtin (r06, formerly inline asm): hipcc sees both, so
+    // no fragment register can be touched before its read has landed.  (Left to itself hipcc
+    // waited lgkmcnt(0) right after issuing every second step's reads.)
     bf16x8 af[2][2] = {}, bf[2][4] = {};
     auto frags = [&](int t, int b) {
       const int tap = t >> 1, dy = tap / 3, dx = tap - (tap / 3) * 3;
@@ -186,16 +182,16 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
         const int pix = apix[mi] + dy * SLOTS + dx;
-        ds_read16(af[b][mi], Ib + pix * 64 + ((lc ^ ((aslot[mi] + dx) & 7)) * 8));
+        af[b][mi] = *(const bf16x8*)(Ib + pix * 64 + ((lc ^ ((aslot[mi] + dx) & 7)) * 8));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int co = j * 16 + r16;
-        ds_read16(bf[b][j], Ws + (tap * 64 + co) * 64 + ((lc ^ ((co >> 1) & 7)) * 8));
+        bf[b][j] = *(const bf16x8*)(Ws + (tap * 64 + co) * 64 + ((lc ^ ((co >> 1) & 7)) * 8));
       }
     };
     frags(0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < 18; ++t) {
@@ -208,16 +204,16 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
           for (int j = 0; j < 4; ++j)
             acc[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[t & 1][j], af[t & 1][mi], acc[mi][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // ... and the wait after all of them
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_sched_barrier(0);
     }
 
     // Epilogue straight from registers: per (pixel tile, cout tile) a lane owns 4 adjacent
     // channels of one pixel -> one 8-B store (16 lanes x 32 B per pixel row per instruction).
-    // the prefetch DMA (and the asm residual loads above) have landed: waited for here, before
-    // the stores, and not by a count of younger stores after them -- vmcnt retires a store ahead
-    // of an older load, so a counted wait past stores does not cover the DMA (r03, pairw_bf16)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // The next strip's DMA and the residual loads above have landed: vmcnt(0) here, before the
+    // stores, so the wait covers nothing but them (as the builtin: hipcc's tracking sees it and
+    // adds no wait of its own before the uses of rv).
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -242,8 +238,9 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     // every wave's next-strip DMA has landed (its wait above) and its reads of buffer cur are done
     // (lgkmcnt(0) ends the k-loop) before buffer cur is refilled; the stores stay in flight
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier: no read of buffer cur^1 above it
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the stores have left before the workgroup ends
 }
 
 // shapes this kernel takes (everything else stays on the implicit GEMM)

@@ -127,13 +127,13 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
   const int G = gridDim.x;
   int strip = xcd_tile(blockIdx.x, G, 1);
   if (strip < nstrips) stage(strip, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weights, bias, first strip
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): weights, bias, first strip
   __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
 
   float* __restrict__ y = (float*)a.y;
   const float* __restrict__ res = (const float*)a.res;
   const float rlow = a.relu ? 0.f : -INFINITY;
-  const unsigned lds0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)crf_smem;
   int cur = 0;
   for (; strip < nstrips; strip += G) {
     const int next = strip + G;
@@ -143,10 +143,11 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
     const int y0 = (strip - img * spi) * TR;
     const long long obase = ((long long)img * H + y0) * RW * C + 16 * g + 4 * q;
     // residual: each wave DMAs the 64 B per pixel it adds (pixel k * 16 + lane / 4, quad lane % 4)
-    // into its own LDS region, so the epilogue needs only this wave's vmcnt.  (Register loads
-    // would be live through the k-loop at 256 VGPRs: an asm load's destination may then be
-    // copied before the data lands, and a compiler-visible one is waited for before the first
-    // MFMA.)
+    // into its own LDS region (in the same array as the strips: a DMA into a second __shared__
+    // array makes hipcc wait vmcnt(0) before the next fragment read), so the epilogue needs only
+    // this wave's vmcnt.  (Register loads would be live through the k-loop at 256 VGPRs: an asm
+    // load's destination may then be copied before the data lands, and a compiler-visible one is
+    // waited for before the first MFMA.)
     const bool has_res = RES && (!ABL || (res && !(abl & 2)));  // the ABL instance runs every layer
     unsigned char* rl = crf_smem + 2 * G_::BUF_BYTES + g * G_::RES_WAVE_BYTES;
     if (has_res) {
@@ -154,26 +155,28 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
       for (int k = 0; k < TILES; ++k)
         dma16(res + obase - 4 * q + (long long)(k * 16 + (lane >> 2)) * C + 4 * (lane & 3), rl + k * 1024);
     }
-    unsigned base[TILES];
+    const unsigned char* base[TILES];
 #pragma unroll
-    for (int i = 0; i < TILES; ++i) base[i] = lds0 + cur * G_::BUF_BYTES + pb[i];
+    for (int i = 0; i < TILES; ++i) base[i] = crf_smem + cur * G_::BUF_BYTES + pb[i];
 
     f32x4 acc[TILES];
 #pragma unroll
     for (int i = 0; i < TILES; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 xb[2][TILES];
-    // B fragments of step group t = (tap t / 4, channel group t % 4): immediate offsets only
-    auto frags_ = [](auto tc, int b, f32x4(&xb)[2][TILES], const unsigned(&base)[TILES], int abl) {
+    // B fragments of step group t = (tap t / 4, channel group t % 4): immediate offsets only.
+    // Plain LDS loads and the s_waitcnt builtin (r06, formerly inline asm, whose asynchronous
+    // register write hipcc cannot see): one lgkmcnt(0) per step group retires the next group's
+    // reads, and hipcc knows it.
+    auto frags_ = [](auto tc, int b, f32x4(&xb)[2][TILES], const unsigned char* const(&base)[TILES], int abl) {
       constexpr int t = decltype(tc)::value;
       constexpr int off = ((t >> 2) / 3 * SLOTS + (t >> 2) % 3) * SLOT_BYTES + 64 * (t & 3);
       if (abl & 16) return;
 #pragma unroll
-      for (int i = 0; i < TILES; ++i)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(xb[b][i]) : "v"(base[i]), "i"(off));
+      for (int i = 0; i < TILES; ++i) xb[b][i] = *(const f32x4*)(base[i] + off);
     };
     auto frags = [&](auto tc, int b) { frags_(tc, b, xb, base, abl); };
     frags(std::integral_constant<int, 0>{}, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
     static_for<36>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
@@ -187,14 +190,15 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[t][e], xb[t & 1][i][e], acc[i], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_sched_barrier(0);
     });
 
-    // this wave's residual DMA and next-strip prefetch have landed: waited for before the stores,
-    // not by a count of younger stores after them (vmcnt retires a store ahead of an older load)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's residual DMA and next-strip prefetch have landed: vmcnt(0) before the stores, so
+    // it waits for nothing else
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");  // the residual's LDS reads stay below the wait
 #pragma unroll
     for (int i = 0; i < TILES; ++i) {
       f32x4 rv = {0.f, 0.f, 0.f, 0.f};
@@ -215,9 +219,10 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
     // every wave's next-strip DMA has landed (the wait above) and its reads of buffer cur are
     // done (lgkmcnt(0) ends the k-loop) before it is refilled; the stores stay in flight
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
     cur ^= 1;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 }
 
 bool conv_rows_f32_ok(const ConvArgs& a) {

@@ -49,7 +49,7 @@ constexpr int PIX = 2 * C;                                     // stored split p
 constexpr int VC = 3 * C;                                      // virtual input channels (hi, lo, hi)
 static_assert(TR * RW == TILES * 16, "strip = 7 pixel tiles");
 static_assert(2 * PLANE_PIECES <= PIECES && PIECES % NW == 0, "DMA pieces");
-static_assert(2 * BUF * 2 <= 163840, "LDS budget");
+static_assert(2 * BUF * 2 + NW * TILES * 1024 <= 163840, "LDS budget");
 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((unsigned)v << 16); }
 __device__ __forceinline__ u16 f2bf(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
@@ -63,7 +63,13 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_base) {
 // loads, 16 no ds_reads, 32 no MFMAs, 64 no stores
 template <bool RES, bool ABL>
 __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrips) {
-  __shared__ __attribute__((aligned(16))) u16 In[2 * BUF];
+  // residual (r06): behind the two strip buffers each wave DMAs the hi and lo halves of its 16
+  // couts of the strip's pixels into a region of its own, [pixel][hi 8 | hi 8 | lo 8 | lo 8]
+  // (64 B), so the epilogue waits only for this wave's vmcnt and no register holds an in-flight
+  // load across the k-loop.  (One array: a DMA into a second __shared__ array made hipcc wait
+  // vmcnt(0) before the strip's first fragment read.)
+  __shared__ __attribute__((aligned(16))) u16 In[2 * BUF + (RES ? NW * TILES * 512 : 0)];
+  unsigned char* const Rs = (unsigned char*)(In + 2 * BUF);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -145,44 +151,48 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
     const int img = strip / spi;
     const int y0 = (strip - img * spi) * TR;
     const long long obase = ((long long)img * H + y0) * RW * PIX;
-    uint2 rh[TILES] = {}, rl[TILES] = {};
-    if (RES && (!ABL || (res && !(abl & 2)))) {  // the ABL instance runs every layer, res or not
+    // residual, DMA'd now so the k-loop hides its latency (r06; it was inline-asm register loads,
+    // whose asynchronous register write hipcc cannot see -- the r05 conv_rowsr_bf16 fault -- and
+    // plain register loads get a vmcnt(0) before the first MFMA at this kernel's register
+    // pressure).  Piece i: pixels 16 i + lane / 4, 16-B part lane & 3 (hi 0-7, hi 8-15, lo 0-7,
+    // lo 8-15 of couts 16 g ..).
+    const bool has_res = RES && (!ABL || (res && !(abl & 2)));  // the ABL instance runs every layer, res or not
+    unsigned char* rw = Rs + (RES ? g * TILES * 1024 : 0);
+    if (has_res) {
 #pragma unroll
       for (int i = 0; i < TILES; ++i) {
-        const u16* src = res + obase + (long long)(i * 16 + r16) * PIX + 16 * g + 4 * q;
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(rh[i]) : "v"(src) : "memory");
-        asm volatile("global_load_dwordx2 %0, %1, off offset:128" : "=v"(rl[i]) : "v"(src) : "memory");
+        const int part = lane & 3;
+        dma16(res + obase + (long long)(i * 16 + (lane >> 2)) * PIX + (part >> 1) * C + 16 * g + 8 * (part & 1), rw + i * 1024);
       }
     }
-    const unsigned Ib = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u16*)(In + cur * BUF);
+    const unsigned char* Ib = (const unsigned char*)(In + cur * BUF);
     unsigned xr[9][2];
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        xr[tap][h] = Ib + ((tap / 3) * SLOTS + tap % 3) * 128 + (((4 * h + q) ^ ((r16 + tap % 3) & 7)) << 4);
+        xr[tap][h] = ((tap / 3) * SLOTS + tap % 3) * 128 + (((4 * h + q) ^ ((r16 + tap % 3) & 7)) << 4);
 
     f32x4 acc[TILES];
 #pragma unroll
     for (int i = 0; i < TILES; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x8 xh[2][TILES] = {}, xl[2][TILES] = {};
-    // one add + the hi and lo reads per tile in one asm, so hipcc cannot hoist the 126
-    // summed addresses out of the unrolled k-loop
+    // plain LDS loads (r06, formerly one inline asm per tile): the tile's offset goes through an
+    // empty asm, so hipcc re-adds it per read instead of hoisting the 126 summed addresses out of
+    // the unrolled k-loop (register pressure), and the lo plane is the read's immediate offset
     auto frags = [&](int t, int b) {
       if (abl & 16) return;
 #pragma unroll
       for (int i = 0; i < TILES; ++i) {
-        unsigned tmp;
-        asm volatile(
-            "v_add_u32 %2, %3, %4\n\t"
-            "ds_read_b128 %0, %2\n\t"
-            "ds_read_b128 %1, %2 offset:%5"
-            : "=v"(xh[b][i]), "=v"(xl[b][i]), "=&v"(tmp)
-            : "v"(pb[i]), "v"(xr[t >> 1][t & 1]), "i"(PLANE_BYTES));
+        unsigned o = pb[i];
+        asm volatile("" : "+v"(o));
+        const unsigned char* pp = Ib + (o + xr[t >> 1][t & 1]);
+        xh[b][i] = *(const bf16x8*)pp;
+        xl[b][i] = *(const bf16x8*)(pp + PLANE_BYTES);
       }
     };
     frags(0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < 18; ++t) {
@@ -198,24 +208,30 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
         for (int i = 0; i < TILES; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[t], xl[b][i], acc[i], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the next step's reads
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // residual and next-strip prefetch landed: waited for before the stores, not by a count of
-    // younger stores after them (vmcnt retires a store ahead of an older load)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's residual DMA and next-strip DMA have landed: vmcnt(0) before the stores, so it
+    // waits for nothing else (as the builtin: hipcc's tracking sees it)
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");  // the residual's LDS reads stay below the wait
 #pragma unroll
     for (int i = 0; i < TILES; ++i) {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][e] + bias[e];
       if constexpr (RES) {  // hi + lo is exact in f32
-        v[0] += bf2f((u16)(rh[i].x & 0xffff)) + bf2f((u16)(rl[i].x & 0xffff));
-        v[1] += bf2f((u16)(rh[i].x >> 16)) + bf2f((u16)(rl[i].x >> 16));
-        v[2] += bf2f((u16)(rh[i].y & 0xffff)) + bf2f((u16)(rl[i].y & 0xffff));
-        v[3] += bf2f((u16)(rh[i].y >> 16)) + bf2f((u16)(rl[i].y >> 16));
+        uint2 rh = {0, 0}, rl = {0, 0};
+        if (has_res) {
+          rh = *(const uint2*)(rw + i * 1024 + r16 * 64 + 8 * q);
+          rl = *(const uint2*)(rw + i * 1024 + r16 * 64 + 32 + 8 * q);
+        }
+        v[0] += bf2f((u16)(rh.x & 0xffff)) + bf2f((u16)(rl.x & 0xffff));
+        v[1] += bf2f((u16)(rh.x >> 16)) + bf2f((u16)(rl.x >> 16));
+        v[2] += bf2f((u16)(rh.y & 0xffff)) + bf2f((u16)(rl.y & 0xffff));
+        v[3] += bf2f((u16)(rh.y >> 16)) + bf2f((u16)(rl.y >> 16));
       }
       u16 hb[4], lb[4];
 #pragma unroll
@@ -228,15 +244,16 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
       const uint2 lv = make_uint2((unsigned)lb[0] | ((unsigned)lb[1] << 16), (unsigned)lb[2] | ((unsigned)lb[3] << 16));
       u16* dst = y + obase + (long long)(i * 16 + r16) * PIX + 16 * g + 4 * q;
       if (abl & 64) continue;
-      asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(hv) : "memory");
-      asm volatile("global_store_dwordx2 %0, %1, off offset:128" ::"v"(dst), "v"(lv) : "memory");
+      *(uint2*)dst = hv;  // compiler-visible stores (r06): hipcc's hazard recognizer guards their data VGPRs
+      *(uint2*)(dst + 64) = lv;
     }
     // every wave's next-strip DMA has landed (the wait above) and its reads of buffer cur are
     // done (lgkmcnt(0) ends the k-loop) before it is refilled; the stores stay in flight
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
     cur ^= 1;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 }
 
 bool conv_rows_x3_ok(const ConvArgs& a) {

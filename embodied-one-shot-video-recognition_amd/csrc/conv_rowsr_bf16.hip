@@ -200,7 +200,7 @@ __global__ __launch_bounds__(64 * R1_NW, 1) void conv_rowsr_bf16_kernel(ConvArgs
       const int nt = ph + 1 < P::NPH ? P::TPP : P::WT - t0;         // and its tile count
       // residual of this pass's pixels, loaded now so the k-loop hides its latency.  Plain loads:
       // hipcc counts them (and the LDS-DMA pieces issued after them) in its vmcnt before the first
-      // use.  (Inline-asm loads, as conv_rows_bf16 has them, hide the asynchronous register write
+      // use.  (Inline-asm loads, as conv_rows_bf16 had them until r06, hide the asynchronous register write
       // from the compiler: here it copied the not-yet-loaded values out right after the asm and
       // reused a load's destination pair as the next address -- a memory fault, r05.)
       uint2 rv[RV][2];

@@ -395,3 +395,33 @@ def test_row_kernel_lds_layouts_conflict_free():
     assert sim.sim(28, 128, 256, c128, 7, 1) == (4, 4.0)
     assert sim.sim(32, 128, 256, c128, 8, 1) == (4, 4.0)
     assert sim.sim(28, 128, 256, c64, 7, 1)[0] > 4
+
+
+def test_no_inline_asm_memory_instructions():
+    """r06 (verdict r05, item 2): no kernel issues a load or store from inline asm.
+
+    An asm load's destination is written asynchronously, which hipcc cannot see: under register
+    pressure it may copy the destination, or reuse it as the next address, before the data lands
+    (the r05 conv_rowsr_bf16 memory fault).  Every VMEM / LDS access is therefore a
+    compiler-visible load / store or builtin; inline asm keeps only wait counts, DPP VALU and empty
+    compiler barriers.  This scans every asm statement's text in the kernel sources."""
+    csrc = os.path.join(REPO, "embodied-one-shot-video-recognition_amd", "csrc")
+    mem = re.compile(r"\b(ds|global|buffer|flat|scratch)_[a-z0-9_]+|\bs_(buffer_)?load")
+    bad = []
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith((".hip", ".h")):
+            continue
+        src = open(os.path.join(csrc, fn)).read()
+        src = re.sub(r"//[^\n]*", "", src)  # comments
+        for m in re.finditer(r"\basm\s*(volatile\s*)?\(", src):
+            # the asm statement up to its closing parenthesis (string literals hold no parentheses
+            # here except inside operand constraints, which are balanced)
+            i, depth = m.end(), 1
+            while depth and i < len(src):
+                depth += {"(": 1, ")": -1}.get(src[i], 0)
+                i += 1
+            text = " ".join(re.findall(r'"((?:[^"\\]|\\.)*)"', src[m.end():i]))
+            text = re.sub(r"\\[nt]", " ", text)  # the asm's own line breaks and tabs
+            if mem.search(text):
+                bad.append(f"{fn}: {text[:80]}")
+    assert not bad, bad
