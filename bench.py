@@ -182,19 +182,22 @@ def measured_traffic(dtype, key):
     from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command at this dtype
     (tools/gpu_traffic.sh; the figure covers exactly the timed region's conv-family launches of the
     profiled run, the same launches its traffic_algorithmic covers).  EOSV_TRAFFIC_PROFILE names a
-    specific file, else the newest matching one.  None unless the workload key, the dtype and the
-    kernel sources (src_sha16 = eosv._lib.source_digest()) all match: counters measured on other
-    kernels are never attached."""
+    specific file, else the newest matching one.  None unless the workload key, the dtype, the
+    kernel sources (src_sha16 = eosv._lib.source_digest()) and the build configuration (lib_kind:
+    the release library, not the profiling or a variant build) all match: counters measured on
+    other kernels are never attached.  (The library's own bytes, lib_sha16, are recorded by
+    tools/traffic_json.py for information only: r05 hashed them into src_sha16, so a rebuild of the
+    same sources detached every profile.)"""
     import glob
-    from eosv._lib import source_digest
+    from eosv._lib import library_kind, source_digest
     paths = [os.environ["EOSV_TRAFFIC_PROFILE"]] if os.environ.get("EOSV_TRAFFIC_PROFILE") else \
         sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True)
-    digest = source_digest()
+    digest, kind = source_digest(), library_kind()
     for path in paths:
         if not os.path.exists(path):
             continue
         d = json.load(open(path))
-        if d.get("key") == key and d.get("src_sha16") == digest and dtype in d:
+        if d.get("key") == key and d.get("src_sha16") == digest and d.get("lib_kind", "release") == kind and dtype in d:
             return d[dtype], os.path.relpath(path, REPO)
     return None, None
 
@@ -206,7 +209,8 @@ def algorithmic_bytes_per_launch(args, arch_mod, dtype, frames, prof):
     pooled map); a bf16 conv1 fused into the previous conv3 launch (pair kernels) adds its bytes
     less its never-read input map (as layer_bounds)."""
     ms, fl, nl = prof
-    layers = arch_mod.conv_launch_bytes(arch_mod.SPECS[args.arch], args.res, args.res, ELEM_BYTES[dtype])
+    spec = arch_mod.SPECS[args.arch]
+    layers = arch_mod.fuse_bneck_bytes(arch_mod.conv_launch_bytes(spec, args.res, args.res, ELEM_BYTES[dtype]), spec, nl)
     total = 0.0
     for i in range(min(len(layers), len(nl))):
         pf, wb, pin = layers[i]
@@ -225,7 +229,8 @@ def layer_bounds(prof, dtype, args, arch_mod, frames):
     frac = sum of floors / sum of measured HIP-event times.  A layer is 'hbm'-bound when the byte
     floor is the larger (R50's 1x1 convs at K = 64..256, the bf16 stage-1 maps)."""
     ms, fl, nl = prof
-    layers = arch_mod.conv_launch_bytes(arch_mod.SPECS[args.arch], args.res, args.res, ELEM_BYTES[dtype])
+    spec = arch_mod.SPECS[args.arch]
+    layers = arch_mod.fuse_bneck_bytes(arch_mod.conv_launch_bytes(spec, args.res, args.res, ELEM_BYTES[dtype]), spec, nl)
     peak = MFMA_PEAK_TF[dtype] * 1e12
     nlay = min(len(ms), len(layers))
     # a conv with no launch of its own but bytes (bf16 bottleneck conv1 fused into the previous

@@ -24,6 +24,22 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("" ::: "memory");
 }
 
+// 128-bit buffer store with an SGPR soffset, followed by one wait state the scheduler cannot fill.
+// A VMEM store wider than 64 bits reads its data VGPRs after issue; hipcc pads a VALU write of
+// them right behind the store only when soffset is an inline constant.  With an SGPR soffset it
+// emits nothing, and on gfx950 that write can win: bneck_bf16_kernel<64,64,false> stored the LDS
+// base a following v_mov put in v152 into one dword of lanes 12/13 (tests/native/bneck_check.cpp,
+// tools/isa_scan.py, which the CPU suite runs over the whole library).  Folding the soffset into
+// the voffset instead costs the 256-channel fused kernels 24-48 B/lane of scratch.
+template <class V>
+__device__ __forceinline__ void store_b128_guarded(V v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 0");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 void set_error(const std::string& msg);
 
 // A/B switches and profiling ablations exist only in the profiling build (`make prof` ->
@@ -189,6 +205,27 @@ int launch_pair1x1r_bf16(const Pair1x1Args& a, hipStream_t s);
 int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128)
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems);
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
+// bneck_bf16.hip (r06): a whole bf16 stage-1 bottleneck block in one launch -- conv1 (1x1 cin -> 64)
+// -> conv2 (3x3 64 -> 64) -> conv3 (1x1 64 -> 256 + residual, or + the folded stride-1 downsample
+// of the block input when cin = 64), and with wn the next block's conv1 (1x1 256 -> 64) -> z
+struct BneckArgs {
+  const void* x;                    // [N][H][W][cin] block input (and residual / downsample input)
+  const void* w1; const float* b1;  // [64][cin] folded conv1
+  const void* w2; const float* b2;  // [64][9 * 64] folded conv2, K (kh, kw, cin)
+  const void* w3; const float* b3;  // [256][64 (+ 64: the downsample)] folded conv3
+  const void* wn; const float* bn;  // [64][256] the next block's folded conv1, or nullptr
+  void* y;                          // [N][H][W][256] block output (may be x itself: in place)
+  void* z;                          // [N][H][W][64] next conv1 output (wn only)
+  int N, H, W, cin;
+  LaunchInfo* plan;                 // non-null: record the grid only
+  const void* res;                  // tail: [N][H][W][256] the residual (the block input)
+};
+bool bneck_bf16_ok(int cin, int W, int H, int next);
+int launch_bneck_bf16(const BneckArgs& a, hipStream_t s);
+// the stage's last block from its conv1 output (x = [N][H][W][64], cin 64, w1 unused): conv2 ->
+// conv3 + res -> y, and the next stage's conv1 (wn [128][256]) -> z [N][H][W][128]
+bool bneck_tail_bf16_ok(int W, int H);
+int launch_bneck_tail_bf16(const BneckArgs& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv

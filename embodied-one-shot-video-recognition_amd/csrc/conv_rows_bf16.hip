@@ -132,6 +132,7 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
   if (strip < nstrips) stage(strip, 0);
   // vmcnt(0) as the builtin (not asm) so the compiler's wait tracking knows the bias loads
   // have landed and does not re-wait for them (draining the in-flight DMA) inside the loop
+  asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
   __builtin_amdgcn_s_waitcnt(0x0f70);
   __builtin_amdgcn_s_barrier();
 
@@ -213,6 +214,7 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
     // The next strip's DMA and the residual loads above have landed: vmcnt(0) here, before the
     // stores, so the wait covers nothing but them (as the builtin: hipcc's tracking sees it and
     // adds no wait of its own before the uses of rv).
+    asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __builtin_amdgcn_sched_barrier(0);  // keep the uses of rv below the wait
 #pragma unroll
@@ -237,9 +239,11 @@ __global__ __launch_bounds__(NT) void conv_rows_bf16_kernel(ConvArgs a, int nstr
       }
     // every wave's next-strip DMA has landed (its wait above) and its reads of buffer cur are done
     // (lgkmcnt(0) ends the k-loop) before buffer cur is refilled; the stores stay in flight
+    asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier: no read of buffer cur^1 above it
   }
+  asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the stores have left before the workgroup ends
 }
 

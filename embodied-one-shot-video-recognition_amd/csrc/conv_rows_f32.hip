@@ -127,6 +127,7 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
   const int G = gridDim.x;
   int strip = xcd_tile(blockIdx.x, G, 1);
   if (strip < nstrips) stage(strip, 0);
+  asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): weights, bias, first strip
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
 
     // this wave's residual DMA and next-strip prefetch have landed: vmcnt(0) before the stores, so
     // it waits for nothing else
+    asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");  // the residual's LDS reads stay below the wait
@@ -218,10 +220,12 @@ __global__ __launch_bounds__(NT) void conv_rows_f32_kernel(ConvArgs a, int nstri
     }
     // every wave's next-strip DMA has landed (the wait above) and its reads of buffer cur are
     // done (lgkmcnt(0) ends the k-loop) before it is refilled; the stores stay in flight
+    asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
     cur ^= 1;
   }
+  asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 }
 

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
   const int G = gridDim.x;
   int strip = xcd_tile(blockIdx.x, G, 1);
   if (strip < nstrips) stage(strip, 0);
+  asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): weights, bias, first strip
   __builtin_amdgcn_s_barrier();
 
@@ -214,6 +215,7 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
 
     // this wave's residual DMA and next-strip DMA have landed: vmcnt(0) before the stores, so it
     // waits for nothing else (as the builtin: hipcc's tracking sees it)
+    asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");  // the residual's LDS reads stay below the wait
@@ -249,10 +251,12 @@ __global__ __launch_bounds__(NT) void conv_rows_x3_kernel(ConvArgs a, int nstrip
     }
     // every wave's next-strip DMA has landed (the wait above) and its reads of buffer cur are
     // done (lgkmcnt(0) ends the k-loop) before it is refilled; the stores stay in flight
+    asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // s_barrier is no compiler-level memory barrier
     cur ^= 1;
   }
+  asm volatile("" ::: "memory");  // neither builtin is a compiler-level memory barrier: no LDS access or DMA crosses it
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 }
 

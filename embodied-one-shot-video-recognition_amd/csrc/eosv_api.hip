@@ -658,13 +658,140 @@ static int run_pair(eosv_handle* h, const Block& b, const Block& nb, const void*
   return rc;
 }
 
+// bf16 stage-1 bottleneck blocks as one launch each (bneck_bf16.hip, r06): conv1 -> conv2 -> conv3
+// with the 64-channel maps kept on the CU.  EOSV_BNECK=0 (profiling build): the r05 path.
+static bool bneck_enabled() {
+  static const bool v = env_switch("EOSV_BNECK", 1) != 0;
+  return v;
+}
+
+static bool bneck_eligible(const eosv_handle* h, const Block& b, int hh, int ww) {
+  if (!bneck_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck) return false;
+  // profiling-build diagnosis switch: EOSV_BNECK=2 fuses only the 256-channel-input blocks, 3 only
+  // block 0 (the 64-channel input with the folded downsample)
+  static const int mode = env_switch("EOSV_BNECK", 1);
+  if ((mode == 2 && b.c1.cin != 256) || (mode == 3 && b.c1.cin != 64)) return false;
+  const Conv &c1 = b.c1, &c2 = b.c2, &c3 = b.c3;
+  if (c1.kh != 1 || c1.stride != 1 || c1.cout != 64 || c2.kh != 3 || c2.stride != 1 || c2.cin != 64 ||
+      c2.cout != 64 || c2.kcm || c3.kh != 1 || c3.cin != 64 || c3.cout != 256)
+    return false;
+  if (b.has_ds ? !(b.fuse_ds && b.ds.stride == 1 && c1.cin == 64 && c3.kds == 64) : c1.cin != 256) return false;
+  return bneck_bf16_ok(c1.cin, ww, hh, 0);
+}
+
+// block bi is its stage's last block (stage_end holds the cumulative block counts)
+static bool last_in_stage(const eosv_handle* h, size_t bi) {
+  for (size_t li = 0; li < 4; ++li)
+    if (bi + 1 == h->stage_end[li]) return true;
+  return false;
+}
+
+// block b as one bneck_bf16 launch: x -> y, and with nb the next block's conv1 on y -> z
+static int run_bneck(eosv_handle* h, const Block& b, const Block* nb, const void* x, void* y, void* z, int B, int hh,
+                     int ww, hipStream_t s) {
+  BneckArgs a{};
+  a.x = x;
+  a.w1 = b.c1.w;
+  a.b1 = b.c1.b;
+  a.w2 = b.c2.w;
+  a.b2 = b.c2.b;
+  a.w3 = b.c3.w;
+  a.b3 = b.c3.b;
+  a.wn = nb ? nb->c1.w : nullptr;
+  a.bn = nb ? nb->c1.b : nullptr;
+  a.y = y;
+  a.z = z;
+  a.N = B;
+  a.H = hh;
+  a.W = ww;
+  a.cin = b.c1.cin;
+  const double M = (double)B * hh * ww;
+  const double flops = 2.0 * M * (64.0 * b.c1.cin + 9.0 * 64 * 64 + 256.0 * (64 + b.c3.kds) + (nb ? 64.0 * 256 : 0.0));
+  if (h->planning) {
+    LaunchInfo li{};
+    a.plan = &li;
+    const int prc = launch_bneck_bf16(a, s);
+    if (prc == EOSV_OK) add_plan_cost(h, li, flops);
+    return prc;
+  }
+  poison_lds(s);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->prof) {
+    e0 = prof_event(h);
+    e1 = prof_event(h);
+    if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
+    EOSV_HIP_CHECK(hipEventRecord(e0, s));
+  }
+  const int rc = launch_bneck_bf16(a, s);
+  if (h->prof && rc == EOSV_OK) {
+    EOSV_HIP_CHECK(hipEventRecord(e1, s));
+    h->recs.push_back({b.c1.id, e0, e1, flops});  // profiled as the block's conv1 layer, with every conv's FLOPs
+  }
+  return rc;
+}
+
+// the stage's last bf16 stage-1 block, whose conv1 output a bneck_bf16 NEXT launch wrote, with the
+// next stage's conv1 (1x1 256 -> 128): bneck_tail_bf16 (r06).  EOSV_BNECK_TAIL=0 (profiling build):
+// conv_rows_bf16 + pair1x1r_bf16 as in r05.
+static bool bneck_tail_eligible(const eosv_handle* h, const Block& b, const Block& nb, int hh, int ww) {
+  static const bool on = env_switch("EOSV_BNECK_TAIL", 1) != 0;
+  if (!on || !bneck_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || b.has_ds || !nb.bottleneck) return false;
+  const Conv &c2 = b.c2, &c3 = b.c3, &n1 = nb.c1;
+  return c2.kh == 3 && c2.stride == 1 && c2.cin == 64 && c2.cout == 64 && !c2.kcm && c3.kh == 1 && c3.cin == 64 &&
+         c3.cout == 256 && b.c1.cout == 64 && n1.kh == 1 && n1.stride == 1 && n1.cin == 256 && n1.cout == 128 &&
+         bneck_tail_bf16_ok(ww, hh);
+}
+
+static int run_bneck_tail(eosv_handle* h, const Block& b, const Block& nb, const void* t1, const void* x, void* y,
+                          void* z, int B, int hh, int ww, hipStream_t s) {
+  BneckArgs a{};
+  a.x = t1;
+  a.res = x;
+  a.w2 = b.c2.w;
+  a.b2 = b.c2.b;
+  a.w3 = b.c3.w;
+  a.b3 = b.c3.b;
+  a.wn = nb.c1.w;
+  a.bn = nb.c1.b;
+  a.y = y;
+  a.z = z;
+  a.N = B;
+  a.H = hh;
+  a.W = ww;
+  a.cin = 64;
+  const double M = (double)B * hh * ww;
+  const double flops = 2.0 * M * (9.0 * 64 * 64 + 256.0 * 64 + 128.0 * 256);
+  if (h->planning) {
+    LaunchInfo li{};
+    a.plan = &li;
+    const int prc = launch_bneck_tail_bf16(a, s);
+    if (prc == EOSV_OK) add_plan_cost(h, li, flops);
+    return prc;
+  }
+  poison_lds(s);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->prof) {
+    e0 = prof_event(h);
+    e1 = prof_event(h);
+    if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
+    EOSV_HIP_CHECK(hipEventRecord(e0, s));
+  }
+  const int rc = launch_bneck_tail_bf16(a, s);
+  if (h->prof && rc == EOSV_OK) {
+    EOSV_HIP_CHECK(hipEventRecord(e1, s));
+    h->recs.push_back({b.c2.id, e0, e1, flops});  // profiled as the block's conv2 layer, with conv2, conv3 and the next conv1
+  }
+  return rc;
+}
+
 // Residual blocks [b0, b1) on x (B frames, hh x ww) using the 4-buffer set `bufs`.  The
 // output of each block lands in place of its residual buffer; when `dst` is given, the last
 // block writes there instead (its residual still comes from `bufs`).
 static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const* bufs, int B, int& hh,
                       int& ww, void* dst, void** xout, bool bf, hipStream_t s) {
   int rc;
-  bool c1_done = false;  // this block's conv1 output is already in fr[0] (fused into the previous pair)
+  bool c1_done = false;    // this block's conv1 output is already in c1buf (fused into the previous launch)
+  void* c1buf = nullptr;
   for (size_t bi = b0; bi < b1; ++bi) {
     const Block& b = h->blocks[bi];
     void* fr[3];
@@ -683,22 +810,49 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
     const void* res = b.fuse_ds ? nullptr : r;
     const void* x2 = b.fuse_ds ? x : nullptr;
     const int s2 = b.has_ds ? b.ds.stride : 1;
+    // the first buffer that is not `a` (and not `c`): where a next block's conv1 output goes
+    auto first_not = [&](const void* a, const void* c, const void* d = nullptr) {
+      for (int k = 0; k < 4; ++k)
+        if (bufs[k] != a && bufs[k] != c && bufs[k] != d) return bufs[k];
+      return (void*)nullptr;
+    };
+    const Block* nb = bi + 1 < b1 ? &h->blocks[bi + 1] : nullptr;
     if (!b.bottleneck) {
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
       if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) return rc;
+    } else if (!c1_done && nb && !last_in_stage(h, bi) && bneck_eligible(h, b, hh, ww)) {
+      // the whole block in one launch (not the stage's last block: that one takes the tail kernel
+      // or conv2 + the pair with the next stage's conv1); when the next block is that last one,
+      // its conv1 too (into the first buffer that is not y: x itself only for a downsample block,
+      // whose 64-channel input pixels are each read before their z is written)
+      const bool next = last_in_stage(h, bi + 1) && nb->bottleneck && nb->c1.kh == 1 && nb->c1.cin == 256 &&
+                        nb->c1.cout == 64 && nb->c1.stride == 1;
+      void* z = next ? first_not(y, nullptr) : nullptr;
+      if ((rc = run_bneck(h, b, next ? nb : nullptr, x, y, z, B, hh, ww, s))) return rc;
+      c1_done = next;
+      c1buf = z;
+    } else if (c1_done && nb && last_in_stage(h, bi) && y == x && bneck_tail_eligible(h, b, *nb, hh, ww)) {
+      // the stage's last block from its conv1 output: conv2 -> conv3 (+ x) -> y = x in place, and the
+      // next stage's conv1 -> a buffer that is neither y nor the conv1 output being read
+      void* z = first_not(y, c1buf);
+      if ((rc = run_bneck_tail(h, b, *nb, c1buf, x, y, z, B, hh, ww, s))) return rc;
+      c1buf = z;  // c1_done stays true
     } else {
-      if (!c1_done && (rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
-      if ((rc = run_conv(h, b.c2, fr[0], B, hh, ww, nullptr, fr[1], true, bf, s))) return rc;
-      // the next block's conv1 lands in its fr[0]: the first buffer that is not its input y
-      const Block* nb = bi + 1 < b1 ? &h->blocks[bi + 1] : nullptr;
-      void* z = nullptr;
-      for (int k = 0; k < 4 && !z; ++k)
-        if (bufs[k] != y) z = bufs[k];
+      void* t1 = c1_done ? c1buf : fr[0];  // conv1 output
+      if (!c1_done && (rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, t1, true, bf, s))) return rc;
+      void* t2 = t1 == fr[0] ? fr[1] : fr[0];  // conv2 output: a buffer that is neither x nor t1
+      if ((rc = run_conv(h, b.c2, t1, B, hh, ww, nullptr, t2, true, bf, s))) return rc;
+      // the next block's conv1 lands in the first buffer that the pair does not read (x, t2) or write
+      // (y); t1 was consumed by conv2.  (Until r06: the first buffer that is not y, so with conv1
+      // outputs placed by the fused stage-1 launches the stage-2 entry pair found x there and fell
+      // back to two launches.)
+      void* z = first_not(y, x, t2);
       const long long M = (long long)B * ho * wo;
-      c1_done = pair_ok(h, b, nb, M) && y != dst && z != x && z != fr[1];
+      c1_done = z && pair_ok(h, b, nb, M) && y != dst && z != x && z != t2;
       if (c1_done) {
-        if ((rc = run_pair(h, b, *nb, fr[1], x2, res, y, z, M, s, ho, wo, hh, ww))) return rc;
-      } else if ((rc = run_conv(h, b.c3, fr[1], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) {
+        if ((rc = run_pair(h, b, *nb, t2, x2, res, y, z, M, s, ho, wo, hh, ww))) return rc;
+        c1buf = z;
+      } else if ((rc = run_conv(h, b.c3, t2, B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) {
         return rc;
       }
     }
@@ -1046,7 +1200,9 @@ int eosv_profile_enable(eosv_handle* h, int enable) {
   if (!h) return set_error("eosv_profile_enable: null handle"), EOSV_ERR_ARG;
   // the window's first / last dispatch (null stream, one wave, no memory access): a kernel trace or
   // PMC pass of the same command finds exactly the profiled launches between the two markers
-  // (tools/traffic_json.py), instead of counting dispatches back from the end of the run
+  // (tools/traffic_json.py), instead of counting dispatches back from the end of the run.  On the
+  // handle's device (its null stream), as every other entry point that launches
+  EOSV_HIP_CHECK(hipSetDevice(h->d.device));
   if (enable && !h->prof) {
     hipLaunchKernelGGL(profile_window_begin_kernel, dim3(1), dim3(64), 0, (hipStream_t)0);
     EOSV_LAUNCH_CHECK();

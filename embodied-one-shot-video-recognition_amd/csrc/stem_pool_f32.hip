@@ -232,7 +232,9 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
   // the offset are wave-uniform (SGPRs), the lane part one VGPR.  The per-tile 64-bit pointers of the
   // plain stores were 14 VGPRs, two of them spilled: two scratch reloads per step, each waiting
   // (vmcnt(0)) for the step's stores issued before it.
-  const int obytes = SPLIT ? 256 : 256;  // bytes per pooled pixel: 64 f32, or 128 bf16 (hi, lo)
+  // bytes per pooled pixel: 64 f32, or (SPLIT) 64 bf16 hi + 64 bf16 lo -- the same 256 B
+  constexpr int obytes = 256;
+  static_assert(64 * 4 == 2 * 64 * 2, "the f32 and split pooled pixels have one size");
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
       (unsigned char*)y + (long long)img * Hq * Wq * obytes, (short)0, Hq * Wq * obytes, 0x00020000);
   const int yvo = (r16 >> 1) * obytes + (SPLIT ? 2 : 4) * (16 * g + 4 * q);  // lane part
@@ -265,8 +267,9 @@ __global__ __launch_bounds__(SPF_NT, 3) void stem_pool_f32_kernel(const float* _
         prev[k][e] = v2;
       }
     // the next step's rows (staged at this step's start) have landed: waited for before the
-    // stores, not by a count of younger stores after them (vmcnt retires a store ahead of an
-    // older load, and a store whose lanes are all past the map may not be issued at all)
+    // stores, not by a count of younger stores after them (a store whose lanes are all past the
+    // map may not be issued at all, so that count is not a constant; loads, stores and LDS-DMA
+    // retire in issue order, MI355X_MICROARCH.md)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < NT; ++k) {

@@ -16,10 +16,11 @@ LIB_PATH = os.environ.get("EOSV_LIBRARY") or os.path.join(PKG_ROOT, "libeosv.so"
 
 def source_digest() -> str:
     """sha256 (16 hex) of the library's sources and build recipe (csrc/*.hip, common.h,
-    include/eosv.h, csrc/Makefile) and of the bytes of the library this process loads (LIB_PATH:
-    libeosv.so, or the EOSV_LIBRARY build): ties a profile (e.g. profiles/*_traffic.json) to the
-    kernels it measured, so a profiling or variant build never passes for the release one;
-    computable on the GPU box, where there is no git history."""
+    include/eosv.h, csrc/Makefile): ties a profile (e.g. profiles/*_traffic.json) to the kernels it
+    measured; computable on the GPU box, where there is no git history.  The library binary is NOT
+    hashed here (r06: a non-reproducible rebuild, or a digest taken before the build, silently
+    detached every profile): which build a profile ran is library_kind(), and its bytes are
+    library_digest(), recorded beside it for information."""
     import glob
     import hashlib
 
@@ -32,11 +33,24 @@ def source_digest() -> str:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
-    h.update(b"library:")
-    if os.path.exists(LIB_PATH):
-        with open(LIB_PATH, "rb") as fh:
-            h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+def library_kind() -> str:
+    """The build configuration this process loads: "release" (libeosv.so), else the library's file
+    name (libeosv_prof.so: the profiling build with its A/B switches; libeosv_<variant>.so)."""
+    name = os.path.basename(LIB_PATH)
+    return "release" if name == "libeosv.so" else name
+
+
+def library_digest() -> str:
+    """sha256 (16 hex) of the bytes of the library this process loads ("" before it exists)."""
+    import hashlib
+
+    if not os.path.exists(LIB_PATH):
+        return ""
+    with open(LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
 EOSV_F32, EOSV_BF16, EOSV_F32X3 = 0, 1, 2

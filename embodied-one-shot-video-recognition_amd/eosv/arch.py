@@ -146,6 +146,49 @@ def conv_layer_bytes(spec: ResNetSpec, H: int = 224, W: int = 224, elem: int = 4
     return layers
 
 
+def block_layer_ids(spec: ResNetSpec):
+    """(conv1, conv2, conv3 or None, downsample or None) layer ids of every residual block, in the
+    native plan's order (stem = 0; csrc/eosv_api.hip build_plan)."""
+    out, i = [], 1
+    inplanes = 64
+    for li, (planes, n) in enumerate(zip((64, 128, 256, 512), spec.layers)):
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            cout = planes * spec.expansion
+            ds = bi == 0 and (s != 1 or inplanes != cout)
+            if spec.block == "basic":
+                ids = (i, i + 1, None)
+                i += 2
+            else:
+                ids = (i, i + 1, i + 2)
+                i += 3
+            out.append(ids + ((i,) if ds else (None,)))
+            i += 1 if ds else 0
+            inplanes = cout
+    return out
+
+
+def fuse_bneck_bytes(layers, spec: ResNetSpec, nl):
+    """conv_launch_bytes adjusted for the blocks the native forward ran as ONE launch
+    (bneck_bf16.hip, r06): recognised from the profile itself -- conv1 launched, conv2 and conv3
+    not.  Such a launch reads the block input once (conv1's input is also conv3's residual, or the
+    folded stride-1 downsample's input: the same pixels, read once) and writes the block output; its
+    64-channel maps (conv1's and conv2's outputs) never reach HBM.  Its entry moves onto conv1's id,
+    with all three weight matrices; conv2 / conv3 become empty.  (A next conv1 fused into it keeps the
+    generic rule: an unlaunched conv's bytes less its input map join the previous launch.)"""
+    L = [tuple(x) for x in layers]
+    for c1, c2, c3, _ in block_layer_ids(spec):
+        if c3 is None or c3 >= len(L) or c3 >= len(nl):
+            continue
+        if nl[c1] and not nl[c2] and not nl[c3]:
+            pf1, wb1, pin1 = L[c1]
+            pf2, wb2, pin2 = L[c2]
+            pf3, wb3, pin3 = L[c3]
+            L[c1] = (pf1 - pin2 + pf3 - pin3 - pin1, wb1 + wb2 + wb3, pin1)
+            L[c2] = L[c3] = (0, 0, 0)
+    return L
+
+
 def conv_launch_bytes(spec: ResNetSpec, H: int = 224, W: int = 224, elem: int = 4):
     """Algorithmic HBM bytes per conv launch as the native forward runs it, in the plan's layer-id
     order (conv_layer_bytes' list, same indices): the fused stem + maxpool reads the caller's f32

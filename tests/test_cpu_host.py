@@ -403,8 +403,8 @@ def test_no_inline_asm_memory_instructions():
     An asm load's destination is written asynchronously, which hipcc cannot see: under register
     pressure it may copy the destination, or reuse it as the next address, before the data lands
     (the r05 conv_rowsr_bf16 memory fault).  Every VMEM / LDS access is therefore a
-    compiler-visible load / store or builtin; inline asm keeps only wait counts, DPP VALU and empty
-    compiler barriers.  This scans every asm statement's text in the kernel sources."""
+    compiler-visible load / store or builtin; inline asm keeps only wait counts, DPP VALU, s_nop
+    and empty compiler barriers.  This scans every asm statement's text in the kernel sources."""
     csrc = os.path.join(REPO, "embodied-one-shot-video-recognition_amd", "csrc")
     mem = re.compile(r"\b(ds|global|buffer|flat|scratch)_[a-z0-9_]+|\bs_(buffer_)?load")
     bad = []
@@ -425,3 +425,49 @@ def test_no_inline_asm_memory_instructions():
             if mem.search(text):
                 bad.append(f"{fn}: {text[:80]}")
     assert not bad, bad
+
+
+def test_no_store_data_hazard_in_library():
+    """r06: no 128-/96-bit VMEM store in the built library is directly followed by a VALU write of
+    its data VGPRs.  hipcc pads that pair only for an inline-constant soffset; with an SGPR soffset
+    the write won on gfx950 (bneck_bf16_kernel<64,64,false>: one dword of lanes 12/13 held the
+    next v_mov's LDS base, tests/native/bneck_check.cpp).  Disassembles every gfx950 code object of
+    the release and profiling libraries (tools/isa_scan.py)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import isa_scan
+    if not os.path.exists(os.path.join(isa_scan.LLVM, "llvm-objdump")):
+        pytest.skip("no llvm-objdump")
+    pkg = os.path.dirname(_lib.LIB_PATH)
+    libs = [p for p in (os.path.join(pkg, "libeosv.so"), os.path.join(pkg, "libeosv_prof.so")) if os.path.exists(p)]
+    if not libs:
+        pytest.skip("library not built")
+    for lib in libs:
+        n = len(isa_scan.code_objects(lib))
+        assert n > 10, f"{lib}: {n} gfx950 code objects"
+        found = isa_scan.scan(lib)
+        assert not found, found[:4]
+
+
+def test_fused_block_bytes_follow_the_profile():
+    """r06: a stage-1 block run as ONE launch (bneck_bf16.hip: conv1 launched, conv2 / conv3 not) is
+    priced as input map + output map (+ the next conv1's output when that one is fused too) and all
+    its weights; its 64-channel maps never reach HBM.  Blocks launched conv by conv keep their bytes."""
+    from eosv import arch
+
+    spec = arch.SPECS["resnet50"]
+    ids = arch.block_layer_ids(spec)
+    assert ids[0] == (1, 2, 3, 4) and ids[1] == (5, 6, 7, None) and ids[3] == (11, 12, 13, 14)
+    assert sum(len([x for x in b if x is not None]) for b in ids) + 1 == len(arch.conv_launch_bytes(spec))
+    L = arch.conv_launch_bytes(spec, 224, 224, 2)
+    n = len(L)
+    nl = np.array([1 if L[i][0] else 0 for i in range(n)])
+    nl[[2, 3, 6, 7, 8]] = 0  # blocks 0 and 1 fused (block 1 with block 2's conv1)
+    F = arch.fuse_bneck_bytes(L, spec, nl)
+    px = 56 * 56
+    assert F[1][0] == (px * 64 + px * 256) * 2  # block 0: X0 in, Y0 out (the downsample reads X0 too)
+    assert F[1][1] == (64 * 64 + 64 * 576 + 256 * 128) * 2
+    assert F[5][0] == (px * 256 + px * 256) * 2  # block 1: Y0 in (also the residual), Y1 out
+    assert F[2] == F[3] == F[6] == F[7] == (0, 0, 0)
+    assert F[8] == L[8] and F[9:] == L[9:]  # block 2's conv1 keeps its entry (the generic next-conv1 rule)
+    # blocks run conv by conv: unchanged
+    assert arch.fuse_bneck_bytes(L, spec, np.array([1 if L[i][0] else 0 for i in range(n)])) == L

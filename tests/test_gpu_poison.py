@@ -37,13 +37,17 @@ def test_r05_kernels_bitwise_equal_r04(switch, name, tmp_path):
     EOSV_BF16_ROWSR: conv_rowsr_bf16 (3x3 row strips, weights in registers) against conv_rows_bf16
     (stage 1 at 224), the tap-shift tile (stage 2) and the 128x64 implicit GEMM (stage 1 at 256:
     resnet101:256 = config 5's shapes)."""
+    _switch_stage_maps_equal(switch, name, tmp_path, "r05", "r04")
+
+
+def _switch_stage_maps_equal(switch, name, tmp_path, new="new", old="old", dtype="bf16"):
     if not os.path.exists(LIB):
         pytest.fail("libeosv_prof.so missing: run __graft_entry__.build()")
     outs = []
     for v in ("1", "0"):
         out = str(tmp_path / f"{switch}_{v}.pt")
         env = dict(os.environ, EOSV_LIBRARY=LIB, **{switch: v})
-        r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "ws_diff.py"), "save", out, name, "bf16"],
+        r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "ws_diff.py"), "save", out, name, dtype],
                            env=env, capture_output=True, text=True, timeout=200)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(out)
@@ -52,4 +56,15 @@ def test_r05_kernels_bitwise_equal_r04(switch, name, tmp_path):
     if not all(torch.equal(u, v) for u, v in zip(a, b)):
         cmp = subprocess.run([sys.executable, os.path.join(REPO, "tools", "ws_diff.py"), "cmp", outs[0], outs[1]],
                              capture_output=True, text=True, timeout=120).stdout
-        pytest.fail(f"stage maps differ between the r05 and r04 kernels ({switch}):\n{cmp}")
+        pytest.fail(f"stage maps differ between the {new} and {old} kernels ({switch}):\n{cmp}")
+
+
+@pytest.mark.parametrize("name", ["resnet50", "resnet50:224:601", "resnet101:256", "resnet101:256:300"])
+def test_bneck_bitwise_equal_unfused(name, tmp_path):
+    """r06: the whole-block stage-1 kernel (bneck_bf16.hip: conv1 -> conv2 -> conv3 in one launch,
+    plus the next block's conv1) against the r05 path it replaces (EOSV_BNECK=0: the 1x1 conv,
+    conv_rows_bf16 / conv_rowsr_bf16 and the pair kernels): every stage map bitwise equal, at 224
+    (R50: 56x56 maps, a phantom tile per wave 3) and 256 (R101: 64x64), with one image per
+    workgroup (37 frames) and with 2-3 images per workgroup (601 / 300 frames on 256 CUs: the
+    stream crosses images through the zero step, ragged image counts per workgroup)."""
+    _switch_stage_maps_equal("EOSV_BNECK", name, tmp_path, "bneck", "r05 stage-1")

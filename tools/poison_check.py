@@ -4,7 +4,9 @@ each launch.  A kernel whose valid outputs read activation rows or LDS words nob
 gives NaN or different features on the FIRST run, independent of timing, so one pass over the
 batch sizes below is the check (no repetition).  Per case: stage maps 0-4 and features, bitwise.
 
-  EOSV_LIBRARY=.../libeosv_prof.so python tools/poison_check.py [arch,...] [dtype,...] [frames,...]
+  EOSV_LIBRARY=.../libeosv_prof.so python tools/poison_check.py [arch[:res],...] [dtype,...] [frames,...]
+
+(arch:res, e.g. resnet101:256, runs that frame size; 224 otherwise.)
 """
 import os
 import sys
@@ -30,14 +32,15 @@ def run(bb, x, mode):
 
 MODE = int(os.environ.get("POISON_MODE", "3"))  # EOSV_POISON bits of the poisoned run
 fails = 0
-for name in archs:
+for spec_name in archs:
+    name, res = (spec_name.split(":")[0], int(spec_name.split(":")[1])) if ":" in spec_name else (spec_name, 224)
     sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
     for dtype in dtypes:
         nmax = max(counts)
-        bb = engine.Backbone(name, dtype, 224, 224, max_frames=nmax)
+        bb = engine.Backbone(name, dtype, res, res, max_frames=nmax)
         bb.load_state_dict(sd)
         for nf in counts:
-            x = torch.randn(nf, 3, 224, 224, generator=torch.Generator().manual_seed(nf)).cuda()
+            x = torch.randn(nf, 3, res, res, generator=torch.Generator().manual_seed(nf)).cuda()
             plain = run(bb, x, 0)
             pois = run(bb, x, MODE)
             bad = []
@@ -47,14 +50,14 @@ for name in archs:
                     fr = torch.nonzero(torch.isnan(d).any(1) | (d.nan_to_num(1.0).amax(1) > 0)).flatten().tolist()
                     bad.append(f"{'stage %d' % i if i < 5 else 'features'}: frames {fr[:8]}{'...' if len(fr) > 8 else ''}"
                                f" nan {int(torch.isnan(b).sum())}")
-            print(f"{name} {dtype} frames {nf}: {'OK' if not bad else 'DIFFERS ' + '; '.join(bad)}", flush=True)
+            print(f"{spec_name} {dtype} frames {nf}: {'OK' if not bad else 'DIFFERS ' + '; '.join(bad)}", flush=True)
             fails += bool(bad)
         # multi-chunk: the same frames through a handle that holds fewer than them
         if nmax > 8:
             bb.close()
-            bb = engine.Backbone(name, dtype, 224, 224, max_frames=nmax // 3)
+            bb = engine.Backbone(name, dtype, res, res, max_frames=nmax // 3)
             bb.load_state_dict(sd)
-            x = torch.randn(nmax, 3, 224, 224, generator=torch.Generator().manual_seed(99)).cuda()
+            x = torch.randn(nmax, 3, res, res, generator=torch.Generator().manual_seed(99)).cuda()
             os.environ["EOSV_POISON"] = "0"
             a = bb.forward(x)
             os.environ["EOSV_POISON"] = str(MODE)
@@ -62,7 +65,7 @@ for name in archs:
             torch.cuda.synchronize()
             os.environ["EOSV_POISON"] = "0"
             ok = torch.equal(a, b)
-            print(f"{name} {dtype} frames {nmax} in chunks of <= {nmax // 3}: {'OK' if ok else 'DIFFERS'}", flush=True)
+            print(f"{spec_name} {dtype} frames {nmax} in chunks of <= {nmax // 3}: {'OK' if ok else 'DIFFERS'}", flush=True)
             fails += not ok
         bb.close()
 print(f"poison_check: {fails} failing case(s)")

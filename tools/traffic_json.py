@@ -1,7 +1,8 @@
 """Conv-family HBM traffic per launch from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
 one pair per dtype (tools/gpu_traffic.sh), written as profiles/<tag>_traffic.json.  bench.py and
 tools/bench_configs.py attach it as roofline.traffic only to the same workload (key) on the same
-kernel sources and library (src_sha16).
+kernel sources (src_sha16), the build configuration (lib_kind) and, for information, the library's
+bytes (lib_sha16).
 
   python tools/traffic_json.py <out.json> <dir> <dtype> [<dtype> ...]
 
@@ -14,7 +15,8 @@ dispatches inside it, and their number must equal the line's roofline.conv_launc
 its traffic_algorithmic covers) -- nothing is back-filled from warmup or setup dispatches.  The
 family is every kernel the library's conv profile records cover (the stems, the implicit GEMMs,
 the row / strip kernels and the fused pairs: names starting conv_, stem_pool_, pair1x1 (both
-pair1x1_bf16 and the r04 pair1x1r_bf16) or pairw_); the other kernels of the window (clip
+pair1x1_bf16 and the r04 pair1x1r_bf16), pairw_ or bneck_ (the r06 whole-block stage-1 kernel));
+the other kernels of the window (clip
 embedding, matching) are listed under "other_in_window".
 
 HBM bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: rocprofv3 reports KiB and on gfx950
@@ -27,9 +29,9 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "embodied-one-shot-video-recognition_amd"))
-from eosv._lib import source_digest  # noqa: E402
+from eosv._lib import library_digest, library_kind, source_digest  # noqa: E402
 
-FAMILY = ("conv_", "stem_pool_", "pair1x1", "pairw_")
+FAMILY = ("conv_", "stem_pool_", "pair1x1", "pairw_", "bneck_")
 BEGIN, END = "profile_window_begin_kernel", "profile_window_end_kernel"
 
 
@@ -111,7 +113,7 @@ def main():
            "formula": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per launch over the conv-family dispatches inside "
                       "the profiled run's timed window (between the library's window marker kernels); their count "
                       "equals roofline.conv_launches",
-           "src_sha16": source_digest(), "kernels": {}}
+           "src_sha16": source_digest(), "lib_kind": library_kind(), "lib_sha16": library_digest(), "kernels": {}}
     for dt in dtypes:
         key, res, kb = one_dtype(d, dt)
         if doc.get("key", key) != key:

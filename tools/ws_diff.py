@@ -11,12 +11,15 @@ sys.path.insert(0, os.path.join(REPO, "embodied-one-shot-video-recognition_amd")
 
 if sys.argv[1] == "save":
     from eosv import arch, engine, synth  # noqa: E402
-    name = sys.argv[3] if len(sys.argv) > 3 else "resnet50"  # arch, or arch:res (e.g. resnet101:256)
-    name, res = (name.split(":")[0], int(name.split(":")[1])) if ":" in name else (name, 224)
+    name = sys.argv[3] if len(sys.argv) > 3 else "resnet50"  # arch, arch:res or arch:res:frames (e.g. resnet101:256)
+    parts = name.split(":")
+    name = parts[0]
+    res = int(parts[1]) if len(parts) > 1 else 224
+    nf = int(parts[2]) if len(parts) > 2 else 37
     dtype = sys.argv[4] if len(sys.argv) > 4 else "bf16"
     sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
-    x = torch.randn(37, 3, res, res, generator=torch.Generator().manual_seed(5)).cuda()
-    bb = engine.Backbone(name, dtype, res, res, max_frames=37)
+    x = torch.randn(nf, 3, res, res, generator=torch.Generator().manual_seed(5)).cuda()
+    bb = engine.Backbone(name, dtype, res, res, max_frames=nf)
     bb.load_state_dict(sd)
     outs = [bb.probe(x, s).float().cpu() for s in range(5)]
     torch.save(outs, sys.argv[2])
