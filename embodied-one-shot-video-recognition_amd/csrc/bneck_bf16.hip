@@ -48,10 +48,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
-__device__ __forceinline__ float lo_f(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-__device__ __forceinline__ unsigned f2bf(float f) { return (unsigned)__bfloat16_as_ushort(__float2bfloat16(f)); }
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ (row & 7)) * 8; }
+using epi::bf2_f;
+using epi::f32x2;
+using epi::pair_of;
+using epi::relu_bf2;
 // The 1x1 convs read their weight rows in pair1x1r_bf16's permuted order: MFMA tile i, row t (0..15)
 // is channel permrow(i, t) = 32 (i >> 1) + 8 (t >> 2) + 4 (i & 1) + (t & 3) of a 64-channel group, so
 // a lane ends up with channels 8q .. 8q + 7 (tiles 0, 1) and 32 + 8q .. + 7 (tiles 2, 3) of its
@@ -123,6 +124,9 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
   const int poff = live ? pp : SP;
   const int pt2 = live ? pp : 0;            // pixel index for T2 reads (idle: any valid pixel)
   const int H = a.H;
+  // profiling-build ablations (EOSV_BNECK_ABL; results wrong): 1 no conv1 MFMAs, 2 no conv2, 4 no
+  // conv3 / NEXT, 8 loads from empty resources (no HBM reads), 16 stores dropped, 32 no barriers
+  const int abl = EOSV_ABL(a);
   // steps per image: H / 2 row pairs and a zero step, whose conv1 writes two zero rows into the T1
   // ring (the bottom pad row of this image and the top one of the next); a zero step runs the
   // other phases on empty resources (below)
@@ -173,16 +177,16 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
 
   // stream step g's pixels of a [N][H][W][C] tensor: the buffer resource of its 2W pixels (an empty
   // one for a zero step or past this workgroup's last step: loads read 0, stores are dropped)
-  auto step_res = [&](const void* base, int C, int g) {
+  auto step_res = [&](const void* base, int C, int g, bool off = false) {
     const int img = (int)blockIdx.x + (g / NS) * GR;
     const int k = g - (g / NS) * NS;
     const long long p0 = ((long long)img * H + 2 * k) * W;
-    return rsrc((const u16*)base + p0 * C, g < total && k < NS - 1 ? (long long)SP * C * 2 : 0);
+    return rsrc((const u16*)base + p0 * C, g < total && k < NS - 1 && !off ? (long long)SP * C * 2 : 0);
   };
   // input fragments of step g: the wave's tile (k-slice s: channels 32 s + 8q .. of the lane's pixel)
   typedef v4u FragSet[CS];
   auto load_set = [&](int g, FragSet& L) {
-    const __amdgpu_buffer_rsrc_t rx = step_res(a.x, CIN, g);
+    const __amdgpu_buffer_rsrc_t rx = step_res(a.x, CIN, g, abl & 8);
 #pragma unroll
     for (int s = 0; s < CS; ++s) L[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, (poff * CIN + 8 * q) * 2, 64 * s, 0);
   };
@@ -201,6 +205,7 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
     for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < CS; ++s) {
+      if (abl & 1) break;
       bf16x8 af[4];
       {
         int lb = G::W1_OFF + rl * CIN * 2 + ql;
@@ -219,15 +224,9 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
       for (int hh = 0; hh < 2; ++hh) {
         const int c0 = 32 * hh + 8 * q;
         const f32x4 bA = *(const f32x4*)(b1s + c0), bB = *(const f32x4*)(b1s + c0 + 4);
-        const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
         v4u pk;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e0 = 2 * k, e1 = 2 * k + 1;
-          const float v0 = acc[2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-          const float v1 = acc[2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
-        }
+        for (int k = 0; k < 4; ++k) pk[k] = relu_bf2(pair_of(acc[2 * hh], acc[2 * hh + 1], k) + pair_of(bA, bB, k));
         *(v4u*)(dst + (((4 * hh + q) ^ ((ox + 1) & 7)) << 4)) = pk;
       }
     }
@@ -255,6 +254,7 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
     for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t2 = 0; t2 < 18; ++t2) {
+      if (abl & 2) break;
       const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
       bf16x8 bf[4];
 #pragma unroll
@@ -269,10 +269,7 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
     for (int u = 0; u < 4; ++u) {
       if (16 * u + r >= W) continue;
       const int p = OY * W + 16 * u + r;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[u][e] + bias[e], 0.f);
-      const uint2 pk = make_uint2(f2bf(v[0]) | (f2bf(v[1]) << 16), f2bf(v[2]) | (f2bf(v[3]) << 16));
+      const uint2 pk = make_uint2(relu_bf2(acc[u].lo + bias.lo), relu_bf2(acc[u].hi + bias.hi));
       *(uint2*)(T2 + p * 128 + (((2 * cw + (q >> 1)) ^ (p & 7)) << 4) + 8 * (q & 1)) = pk;
     }
   };
@@ -286,8 +283,8 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
   // conv3 of step g (+ NEXT) on the wave's pixel tile, L = step g's input fragments (the residual, or
   // the downsample's input) -> Y (and Z)
   auto conv3 = [&](int g, const FragSet& L) {
-    const __amdgpu_buffer_rsrc_t ry = step_res(a.y, 256, g);
-    const __amdgpu_buffer_rsrc_t rz = step_res(a.z, 64, g);
+    const __amdgpu_buffer_rsrc_t ry = step_res(a.y, 256, g, abl & 16);
+    const __amdgpu_buffer_rsrc_t rz = step_res(a.z, 64, g, abl & 16);
     f32x4 accn[4];
     if constexpr (NEXT) {
 #pragma unroll
@@ -307,6 +304,7 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int s = 0; s < K3 / 32; ++s) {
+          if (abl & 4) break;
           bf16x8 af[2];
           {
             int lb = G::W3_OFF + rl * K3 * 2 + ql;
@@ -324,22 +322,16 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
         // epilogue: + shift (+ residual), ReLU, bf16 -> Y, and the NEXT GEMM's B fragment
         const int c0 = 64 * ch + 32 * hh + 8 * q;
         const f32x4 bA = *(const f32x4*)(b3s + c0), bB = *(const f32x4*)(b3s + c0 + 4);
-        const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
         const v4u rv = DS ? v4u{0, 0, 0, 0} : L[2 * ch + hh];
         v4u pk;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int e0 = 2 * k, e1 = 2 * k + 1;
-          float v0 = acc[e0 >> 2][e0 & 3] + bb[e0];
-          float v1 = acc[e1 >> 2][e1 & 3] + bb[e1];
-          if constexpr (!DS) {
-            v0 += lo_f(rv[k]);
-            v1 += hi_f(rv[k]);
-          }
-          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+          f32x2 v = pair_of(acc[0], acc[1], k) + pair_of(bA, bB, k);
+          if constexpr (!DS) v += bf2_f(rv[k]);
+          pk[k] = relu_bf2(v);
         }
         store_b128_guarded(pk, ry, (poff * 256 + 8 * q) * 2, (ch * 64 + 32 * hh) * 2);
-        if constexpr (NEXT) {
+        if (NEXT && !(abl & 4)) {
           const bf16x8 yf = __builtin_bit_cast(bf16x8, pk);
           bf16x8 aw[4];
           {
@@ -359,15 +351,9 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
       for (int hh = 0; hh < 2; ++hh) {
         const int c0 = 32 * hh + 8 * q;
         const f32x4 bA = *(const f32x4*)(bns + c0), bB = *(const f32x4*)(bns + c0 + 4);
-        const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
         v4u pk;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e0 = 2 * k, e1 = 2 * k + 1;
-          const float v0 = accn[2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-          const float v1 = accn[2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
-        }
+        for (int k = 0; k < 4; ++k) pk[k] = relu_bf2(pair_of(accn[2 * hh], accn[2 * hh + 1], k) + pair_of(bA, bB, k));
         store_b128_guarded(pk, rz, (poff * 64 + 8 * q) * 2, 32 * hh * 2);
       }
     }
@@ -377,10 +363,10 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
   // compiler-level memory barrier -- hipcc may sink an LDS store below both (r06: a T2 store landed
   // after the barrier at W 64, a race that changed 14 of 37 images) -- so an empty asm with a
   // memory clobber fences each side.  lgkmcnt(0): this wave's LDS reads and writes have completed.
-  auto lds_barrier = [] {
+  auto lds_barrier = [&] {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
+    if (!(abl & 32)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
@@ -560,10 +546,7 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_tail_bf16_kernel(BneckArgs a
     for (int u = 0; u < 4; ++u) {
       if (16 * u + r >= W) continue;
       const int p = OY * W + 16 * u + r;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[u][e] + bias[e], 0.f);
-      const uint2 pk = make_uint2(f2bf(v[0]) | (f2bf(v[1]) << 16), f2bf(v[2]) | (f2bf(v[3]) << 16));
+      const uint2 pk = make_uint2(relu_bf2(acc[u].lo + bias.lo), relu_bf2(acc[u].hi + bias.hi));
       *(uint2*)(T2 + p * 128 + (((2 * cw + (q >> 1)) ^ (p & 7)) << 4) + 8 * (q & 1)) = pk;
     }
   };
@@ -608,16 +591,10 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_tail_bf16_kernel(BneckArgs a
         }
         const int c0 = 64 * ch + 32 * hh + 8 * q;
         const f32x4 bA = *(const f32x4*)(b3s + c0), bB = *(const f32x4*)(b3s + c0 + 4);
-        const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
         const v4u rv = R[2 * ch + hh];
         v4u pk;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e0 = 2 * k, e1 = 2 * k + 1;
-          const float v0 = acc[e0 >> 2][e0 & 3] + bb[e0] + lo_f(rv[k]);
-          const float v1 = acc[e1 >> 2][e1 & 3] + bb[e1] + hi_f(rv[k]);
-          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
-        }
+        for (int k = 0; k < 4; ++k) pk[k] = relu_bf2(pair_of(acc[0], acc[1], k) + pair_of(bA, bB, k) + bf2_f(rv[k]));
         store_b128_guarded(pk, ry, (poff * 256 + 8 * q) * 2, (ch * 64 + 32 * hh) * 2);
         const bf16x8 yf = __builtin_bit_cast(bf16x8, pk);
 #pragma unroll
@@ -641,15 +618,9 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_tail_bf16_kernel(BneckArgs a
       for (int hh = 0; hh < 2; ++hh) {
         const int c0 = 64 * g2 + 32 * hh + 8 * q;
         const f32x4 bA = *(const f32x4*)(bns + c0), bB = *(const f32x4*)(bns + c0 + 4);
-        const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
         v4u pk;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e0 = 2 * k, e1 = 2 * k + 1;
-          const float v0 = accn[g2][2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-          const float v1 = accn[g2][2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-          pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
-        }
+        for (int k = 0; k < 4; ++k) pk[k] = relu_bf2(pair_of(accn[g2][2 * hh], accn[g2][2 * hh + 1], k) + pair_of(bA, bB, k));
         store_b128_guarded(pk, rz, (poff * 128 + 8 * q) * 2, (64 * g2 + 32 * hh) * 2);
       }
   };
@@ -732,9 +703,11 @@ int launch_bneck_bf16(const BneckArgs& a, hipStream_t s) {
   if (a.N <= 0 || !bneck_bf16_ok(a.cin, a.W, a.H, next) || !a.x || !a.w1 || !a.b1 || !a.w2 || !a.b2 || !a.w3 ||
       !a.b3 || !a.y || (next && (!a.bn || !a.z)))
     return set_error("bneck_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
-  if (a.cin == 64) return a.W == 56 ? launch_bn<56, 64, false>(a, s) : launch_bn<64, 64, false>(a, s);
-  if (next) return a.W == 56 ? launch_bn<56, 256, true>(a, s) : launch_bn<64, 256, true>(a, s);
-  return a.W == 56 ? launch_bn<56, 256, false>(a, s) : launch_bn<64, 256, false>(a, s);
+  BneckArgs b = a;
+  b.abl = env_switch("EOSV_BNECK_ABL", 0);  // profiling build only (results wrong when set)
+  if (b.cin == 64) return b.W == 56 ? launch_bn<56, 64, false>(b, s) : launch_bn<64, 64, false>(b, s);
+  if (next) return b.W == 56 ? launch_bn<56, 256, true>(b, s) : launch_bn<64, 256, true>(b, s);
+  return b.W == 56 ? launch_bn<56, 256, false>(b, s) : launch_bn<64, 256, false>(b, s);
 }
 
 }  // namespace eosv

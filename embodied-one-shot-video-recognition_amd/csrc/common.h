@@ -24,21 +24,55 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("" ::: "memory");
 }
 
-// 128-bit buffer store with an SGPR soffset, followed by one wait state the scheduler cannot fill.
-// A VMEM store wider than 64 bits reads its data VGPRs after issue; hipcc pads a VALU write of
-// them right behind the store only when soffset is an inline constant.  With an SGPR soffset it
-// emits nothing, and on gfx950 that write can win: bneck_bf16_kernel<64,64,false> stored the LDS
-// base a following v_mov put in v152 into one dword of lanes 12/13 (tests/native/bneck_check.cpp,
-// tools/isa_scan.py, which the CPU suite runs over the whole library).  Folding the soffset into
-// the voffset instead costs the 256-channel fused kernels 24-48 B/lane of scratch.
+// 128-bit buffer store with an SGPR soffset, then one wait state before its data VGPRs can be
+// rewritten.  A VMEM store wider than 64 bits reads its data VGPRs after issue; hipcc pads a VALU
+// write of them right behind the store only when soffset is an inline constant.  With an SGPR
+// soffset it emits nothing, and on gfx950 that write can win: bneck_bf16_kernel<64,64,false> stored
+// the LDS base a following v_mov put in v152 into one dword of lanes 12/13
+// (tests/native/bneck_check.cpp; tools/isa_scan.py checks every store of the library, in the CPU
+// suite).  Folding the soffset into the voffset instead costs the 256-channel fused kernels 24-48
+// B/lane of scratch; a bare s_nop after the store is not enough (the scheduler moved the v_mov
+// above it), sched_barriers around the store cost the epilogue its overlap with the next MFMAs.
 template <class V>
 __device__ __forceinline__ void store_b128_guarded(V v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+#ifdef EOSV_STORE_GUARD_SB  // r06 first form (A/B only: tools/build_variant.sh sbguard -DEOSV_STORE_GUARD_SB)
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 0");
   __builtin_amdgcn_sched_barrier(0);
+#else
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  asm volatile("s_nop 0" ::"v"(v));  // "uses" the data: nothing rewrites its VGPRs before the nop
+#endif
 }
+
+// Packed epilogue arithmetic (r06) for the kernels that keep D = W . X^T accumulators with 8
+// consecutive channels per lane (the fused 1x1 pairs and bneck_bf16): the shift and residual adds as
+// v_pk_add_f32 on (even, odd) channel pairs, bf16(max(v, 0)) as one v_cvt_pk_bf16_f32 and one
+// v_pk_max_i16 with 0 (a bf16 with its sign bit set is a negative int16, so negative values and -0
+// become +0).  Bit for bit the scalar form `bf16(fmaxf(v, 0))` per element (NaN aside), in about
+// half the VALU instructions: that form compiled to one conversion per element plus a shift and an
+// or per pair.
+namespace epi {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned relu_bf2(f32x2 v) {
+  const s16x2 h = __builtin_bit_cast(s16x2, __builtin_convertvector(v, bf16x2));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(h, (s16x2){0, 0}));
+}
+// a bf16x2 word (lo = the even channel) as f32
+__device__ __forceinline__ f32x2 bf2_f(unsigned u) {
+  return (f32x2){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// pair k (channels 2k, 2k + 1 of the lane's 8) of the two accumulators (or shift vectors) A, B
+__device__ __forceinline__ f32x2 pair_of(const f32x4& A, const f32x4& B, int k) {
+  const f32x4 X = k >> 1 ? B : A;
+  return k & 1 ? X.hi : X.lo;
+}
+}  // namespace epi
 
 void set_error(const std::string& msg);
 
@@ -219,6 +253,7 @@ struct BneckArgs {
   int N, H, W, cin;
   LaunchInfo* plan;                 // non-null: record the grid only
   const void* res;                  // tail: [N][H][W][256] the residual (the block input)
+  int abl;                          // profiling-build ablations (EOSV_BNECK_ABL), 0 otherwise
 };
 bool bneck_bf16_ok(int cin, int W, int H, int next);
 int launch_bneck_bf16(const BneckArgs& a, hipStream_t s);

@@ -32,9 +32,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
-__device__ __forceinline__ float lo_f(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-__device__ __forceinline__ unsigned f2bf(float f) { return (unsigned)__bfloat16_as_ushort(__float2bfloat16(f)); }
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ (row & 7)) * 8; }
 // MFMA tile i, row t (0..15) -> channel within the 64-channel group
 __device__ __forceinline__ int permrow(int i, int t) { return 32 * (i >> 1) + 8 * (t >> 2) + 4 * (i & 1) + (t & 3); }
@@ -179,23 +176,17 @@ __global__ __launch_bounds__(64 * PR_NW) void pair1x1r_bf16_kernel(Pair1x1Args a
       for (int hh = 0; hh < 2; ++hh) {
         const int c0 = 64 * ch + 32 * hh + 8 * q;
         const f32x4 bA = *(const f32x4*)(b3s + c0), bB = *(const f32x4*)(b3s + c0 + 4);
-        const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
 #pragma unroll
         for (int tt = 0; tt < NPT; ++tt) {
           const v4u rv = DS ? v4u{0, 0, 0, 0} : rres[ch % NRS][tt][hh];
           v4u pk;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int e0 = 2 * k, e1 = 2 * k + 1;
-            float v0 = acc1[tt][2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-            float v1 = acc1[tt][2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-            if constexpr (!DS) {
-              v0 += lo_f(rv[k]);
-              v1 += hi_f(rv[k]);
-            }
-            pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+          for (int k = 0; k < 4; ++k) {  // packed (common.h, epi): bitwise the scalar form
+            epi::f32x2 v = epi::pair_of(acc1[tt][2 * hh], acc1[tt][2 * hh + 1], k) + epi::pair_of(bA, bB, k);
+            if constexpr (!DS) v += epi::bf2_f(rv[k]);
+            pk[k] = epi::relu_bf2(v);
           }
-          __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * tt) * 256 + 8 * q) * 2, (ch * 64 + 32 * hh) * 2, 0);
+          store_b128_guarded(pk, cur.y, ((pw + 16 * tt) * 256 + 8 * q) * 2, (ch * 64 + 32 * hh) * 2);
           yf[tt][hh] = __builtin_bit_cast(bf16x8, pk);
         }
       }
@@ -226,16 +217,11 @@ __global__ __launch_bounds__(64 * PR_NW) void pair1x1r_bf16_kernel(Pair1x1Args a
         for (int hh = 0; hh < 2; ++hh) {
           const int c0 = 64 * g + 32 * hh + 8 * q;
           const f32x4 bA = *(const f32x4*)(b1s + c0), bB = *(const f32x4*)(b1s + c0 + 4);
-          const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
           v4u pk;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int e0 = 2 * k, e1 = 2 * k + 1;
-            const float v0 = acc2[tt][g][2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-            const float v1 = acc2[tt][g][2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-            pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
-          }
-          __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, ((pw + 16 * tt) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2, 0);
+          for (int k = 0; k < 4; ++k)
+            pk[k] = epi::relu_bf2(epi::pair_of(acc2[tt][g][2 * hh], acc2[tt][g][2 * hh + 1], k) + epi::pair_of(bA, bB, k));
+          store_b128_guarded(pk, cur.z, ((pw + 16 * tt) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2);
         }
     cur = nxt;
   }

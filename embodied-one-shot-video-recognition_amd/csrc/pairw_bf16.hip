@@ -41,9 +41,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_t;
 
-__device__ __forceinline__ float lo_f(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-__device__ __forceinline__ unsigned f2bf(float f) { return (unsigned)__bfloat16_as_ushort(__float2bfloat16(f)); }
 // MFMA tile i, row t (0..15) -> channel within the 64-channel group
 __device__ __forceinline__ int permrow(int i, int t) { return 32 * (i >> 1) + 8 * (t >> 2) + 4 * (i & 1) + (t & 3); }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
@@ -364,24 +361,18 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
             const unsigned char* b3c = ws + P::STAGE_W + (32 * hh + 8 * q) * 4;
             const f32x4 bA = __builtin_bit_cast(f32x4, *(const bf16x8*)b3c);
             const f32x4 bB = __builtin_bit_cast(f32x4, *(const bf16x8*)(b3c + 16));
-            const float bb[8] = {bA[0], bA[1], bA[2], bA[3], bB[0], bB[1], bB[2], bB[3]};
 #pragma unroll
             for (int t = 0; t < NPT; ++t) {
               const v4u rv = DSC ? v4u{0, 0, 0, 0} : rres[u][t][hh];  // ring slot ch & 3 (no residual with DSC)
               v4u pk;
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const int e0 = 2 * k, e1 = 2 * k + 1;  // elements of the lane's 8 couts
-                float v0 = acc1[t][2 * hh + (e0 >> 2)][e0 & 3] + bb[e0];
-                float v1 = acc1[t][2 * hh + (e1 >> 2)][e1 & 3] + bb[e1];
-                if constexpr (!DSC) {
-                  v0 += lo_f(rv[k]);
-                  v1 += hi_f(rv[k]);
-                }
-                pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
+              for (int k = 0; k < 4; ++k) {  // pairs of the lane's 8 couts, packed (common.h, epi): bitwise the scalar form
+                epi::f32x2 v = epi::pair_of(acc1[t][2 * hh], acc1[t][2 * hh + 1], k) + epi::pair_of(bA, bB, k);
+                if constexpr (!DSC) v += epi::bf2_f(rv[k]);
+                pk[k] = epi::relu_bf2(v);
               }
               if (!(abl & 4))
-                __builtin_amdgcn_raw_buffer_store_b128(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2, (ch * 64 + 32 * hh) * 2, 0);
+                store_b128_guarded(pk, cur.y, ((pw + 16 * t) * CEXP + 8 * q) * 2, (ch * 64 + 32 * hh) * 2);
               yf[t][hh] = __builtin_bit_cast(bf16x8, pk);
             }
           }
@@ -400,13 +391,10 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
           const int c0 = 64 * g + 32 * hh + 8 * q;
           v4u pk;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int e0 = 2 * k, e1 = 2 * k + 1;
-            const float v0 = acc2[t][g][2 * hh + (e0 >> 2)][e0 & 3] + b1s[c0 + e0];
-            const float v1 = acc2[t][g][2 * hh + (e1 >> 2)][e1 & 3] + b1s[c0 + e1];
-            pk[k] = f2bf(fmaxf(v0, 0.f)) | (f2bf(fmaxf(v1, 0.f)) << 16);
-          }
-          if (!(abl & 32)) __builtin_amdgcn_raw_buffer_store_b128(pk, cur.z, ((pw + 16 * t) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2, 0);
+          for (int k = 0; k < 4; ++k)
+            pk[k] = epi::relu_bf2(epi::pair_of(acc2[t][g][2 * hh], acc2[t][g][2 * hh + 1], k) +
+                                  (epi::f32x2){b1s[c0 + 2 * k], b1s[c0 + 2 * k + 1]});
+          if (!(abl & 32)) store_b128_guarded(pk, cur.z, ((pw + 16 * t) * C1 + 8 * q) * 2, (64 * g + 32 * hh) * 2);
         }
     cur = nxt;
   }
