@@ -41,6 +41,8 @@ __device__ __forceinline__ void store_b128_guarded(V v, __amdgpu_buffer_rsrc_t r
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 0");
   __builtin_amdgcn_sched_barrier(0);
+#elif defined(EOSV_STORE_GUARD_OFF)  // negative control for the race tests only (tools/build_variant.sh)
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
 #else
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
   asm volatile("s_nop 0" ::"v"(v));  // "uses" the data: nothing rewrites its VGPRs before the nop
@@ -236,7 +238,7 @@ int launch_pair1x1_bf16(const Pair1x1Args& a, hipStream_t s);
 int launch_pair1x1r_bf16(const Pair1x1Args& a, hipStream_t s);
 // pairw_bf16.hip: the same pair for the wide stages (cmid 128 / 256, cexp 512 / 1024): weights
 // streamed through an LDS ring by 64-channel chunks, Y kept in registers; residual blocks only
-int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128)
+int pairw_tile(int cmid, int c1, int cds);  // pixels per pairw round of that shape (128, or 256 at NPT 2)
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems);
 int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s);
 // bneck_bf16.hip (r06): a whole bf16 stage-1 bottleneck block in one launch -- conv1 (1x1 cin -> 64)

@@ -58,7 +58,8 @@ __device__ __forceinline__ void dma16(const unsigned char* src, void* lds) {
 // NPT: 16-pixel tiles per wave, 8 waves (two per SIMD); a round is 128 NPT pixels.  The LDS feeds
 // one 1-KiB weight fragment per MFMA at NPT = 1: per 64-channel chunk the 8 waves read 256 KiB
 // (stage 2) / 512 KiB (stage 3) against 1024 / 2048 MFMA cycles per SIMD, i.e. the LDS read
-// rate, not HBM, bounds the pair.  Only NPT = 1 is built (the static_assert below).
+// rate, not HBM, bounds the pair.  NPT = 2 (r04, restored r06: the stage-2 pair with C1 = 128 on
+// 256-pixel rounds, ~240 VGPRs) reads each fragment once for two pixel tiles.
 // DSC > 0 (block 0 of a stage, r03): conv3's K also holds the folded stride-2 1x1 downsample, DSC
 // more columns read from the previous stage's output x2 at pixel (2 oh, 2 ow) (ConvArgs::x2 of
 // the unfused conv), and there is no residual.
@@ -85,9 +86,7 @@ struct PairW {
   static_assert(STAGE_W % (1024 * NW) == 0 && W3B % 1024 == 0 && PPW >= 2, "DMA pieces");
   static_assert(NCH % 4 == 0, "ring slots / residual ring");
   static_assert(PPW < XS + 2 * G2, "DMA pieces go out one per fragment group, the residual loads after them");
-  // NPT 2 (256-pixel rounds) raced inside the backbone for a reason the r04 / r05 evidence did not
-  // pin (see pairw_tile below): it is not built
-  static_assert(NPT == 1, "pairw_bf16: only 16-pixel tiles per wave (128-pixel rounds)");
+  static_assert(NPT == 1 || (NPT == 2 && DSC == 0 && C1 == 128), "pairw_bf16: NPT 2 only for the stage-2 pair");
 };
 
 // ABL (profiling-only instance, EOSV_CONV_ABL bits; results wrong): 1 no weight DMA, 2 no
@@ -429,14 +428,25 @@ static int launch_pairw(const Pair1x1Args& a, hipStream_t s) {
   return EOSV_OK;
 }
 
-// One 16-pixel tile per wave (128-pixel rounds) for every shape.  The 256-pixel-round form (NPT 2,
-// r04: the stage-2 pair with C1 = 128, 1.45 -> 1.34 ms per launch) was removed in r05: in the
-// backbone it gave run-to-run different R50 / R101 features at 64, 85 and 130 frames per chunk and
-// none at 17, 37, 257, 601 or 1024, and the recorded evidence did not pin a cause (DESIGN.md
-// section 4: the differing frames map to rounds on every XCD; its ISA has the same wait counts,
-// barrier placement and next-round X load as NPT 1's, and the full-drain and MFMA-fence probes did
-// not remove it).  PairW<...>::NPT is therefore fixed at 1 (static_assert above).
-int pairw_tile(int, int, int) { return 128; }
+// 16-pixel tiles per wave of the pair for this shape: NPT 2 (256-pixel rounds) for the stage-2 pair
+// with C1 = 128 (r04: 1.45 -> 1.34 ms per launch), NPT 1 elsewhere.  r04 / r05: NPT 2 gave
+// run-to-run different R50 / R101 features inside the backbone and was removed, cause unpinned.
+// r06 pinned it: the r04 build of pairw_bf16_kernel<128, 512, 128, 2> -- and no NPT 1 instance --
+// holds one Y store (buffer_store_dwordx4, SGPR soffset) directly followed by a v_add_f32 that
+// rewrites one of its data VGPRs (tools/isa_scan.py on the r04 sources), the gfx950 store-data
+// hazard hipcc does not pad (common.h, store_b128_guarded).  Whether the store has read its data
+// by then depends on how busy the memory pipeline is, hence "only inside the backbone".  The
+// stores go through the guard now and the library scan is clean.  EOSV_PAIRW_NPT2=0 (profiling
+// build): NPT 1 everywhere.
+#ifndef EOSV_PAIRW_NPT2_DEF
+#define EOSV_PAIRW_NPT2_DEF 1  // release A/B: tools/build_variant.sh npt1 -DEOSV_PAIRW_NPT2_DEF=0
+#endif
+static int pairw_npt(int cmid, int c1, int cds) {
+  static const int npt2 = env_switch("EOSV_PAIRW_NPT2", EOSV_PAIRW_NPT2_DEF);
+  return npt2 && cmid == 128 && c1 == 128 && cds == 0 ? 2 : 1;
+}
+
+int pairw_tile(int cmid, int c1, int cds) { return 128 * pairw_npt(cmid, c1, cds); }
 
 bool pairw_bf16_ok(int cmid, int cexp, int c1, int cds, long long M, long long cap_elems) {
   if (M <= 0) return false;
@@ -453,7 +463,8 @@ int launch_pairw_bf16(const Pair1x1Args& a, hipStream_t s) {
       (a.cds ? (!a.x2 || a.res || a.Ho <= 0 || a.Wo <= 0 || a.H2 < 2 * a.Ho - 1 || a.W2 < 2 * a.Wo - 1) : (!a.res || a.x2)))
     return set_error("pairw_bf16: unsupported shape"), EOSV_ERR_UNSUPPORTED;
   if (a.cds) return launch_pairw<128, 512, 128, 1, 256>(a, s);
-  if (a.cmid == 128 && a.c1 == 128) return launch_pairw<128, 512, 128, 1>(a, s);
+  if (a.cmid == 128 && a.c1 == 128)
+    return pairw_npt(128, 128, 0) == 2 ? launch_pairw<128, 512, 128, 2>(a, s) : launch_pairw<128, 512, 128, 1>(a, s);
   if (a.cmid == 128) return launch_pairw<128, 512, 256, 1>(a, s);
   return launch_pairw<256, 1024, 256, 1>(a, s);
 }

@@ -259,8 +259,10 @@ def test_backbone_determinism_over_chunk_sizes(name):
     grids end differently (one round per workgroup, 1-2 rounds, several).  r04's stage-2 pair on
     256-pixel rounds gave different features in every repeat at 64 and 130 frames and none at 37,
     257 or 1024 (tools/race_modes.py): the 37-frame test above missed it.
-    That form is removed (r05); the ragged-tail sizes 43 and 257 (stage-2 tail rounds of 48 / 16
-    pixels, 1-2 / 6-7 rounds per workgroup) cover the shipping 128-pixel rounds' tails too."""
+    r06 pinned the cause (a 128-bit store whose data VGPRs the next VALU instruction rewrote, the
+    hazard tools/isa_scan.py now rules out) and restored the 256-pixel rounds
+    with the store guard.  The ragged-tail sizes 43 and 257 (stage-2 tail rounds of 48 / 16
+    pixels, 1-2 / 6-7 rounds per workgroup) cover the rounds' tails too."""
     sd = synth.synth_state_dict(arch.SPECS[name], 64, 0)
     bb = engine.Backbone(name, "bf16", 224, 224, max_frames=257)
     bb.load_state_dict(sd)
