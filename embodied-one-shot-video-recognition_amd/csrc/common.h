@@ -263,6 +263,10 @@ int launch_bneck_bf16(const BneckArgs& a, hipStream_t s);
 // conv3 + res -> y, and the next stage's conv1 (wn [128][256]) -> z [N][H][W][128]
 bool bneck_tail_bf16_ok(int W, int H);
 int launch_bneck_tail_bf16(const BneckArgs& a, hipStream_t s);
+// a bf16 ResNet-18 stage-1 basic block (conv1 3x3 64 -> 64 + ReLU, conv2 3x3 + x + ReLU) in one
+// launch (bblock_bf16.hip, r06): x, w1 / b1, w2 / b2, y (may be x), N, H, W (56 or 64), cin 64
+bool bblock_bf16_ok(int W, int H);
+int launch_bblock_bf16(const BneckArgs& a, hipStream_t s);
 bool conv_rows_f32_ok(const ConvArgs& a);  // conv_rows_f32.hip: f32 stage-1 3x3 64->64 direct conv
 int launch_conv_rows_f32(const ConvArgs& a, hipStream_t s);
 bool conv_rows_x3_ok(const ConvArgs& a);  // conv_rows_x3.hip: f32x3 stage-1 3x3 64->64 direct conv

@@ -731,11 +731,15 @@ static int run_bneck(eosv_handle* h, const Block& b, const Block* nb, const void
 }
 
 // the stage's last bf16 stage-1 block, whose conv1 output a bneck_bf16 NEXT launch wrote, with the
-// next stage's conv1 (1x1 256 -> 128): bneck_tail_bf16 (r06).  EOSV_BNECK_TAIL=0 (profiling build):
-// conv_rows_bf16 + pair1x1r_bf16 as in r05.
+// next stage's conv1 (1x1 256 -> 128): bneck_tail_bf16 (r06).  Default only at 64x64 maps (R101 at
+// 256: stage 1 4.54 -> 4.47 ms per chunk); at 56x56 the two-launch path (conv_rows_bf16 +
+// pair1x1r_bf16) is faster (R50 at the C2 shape: 10.00 vs 10.21-10.28 ms, 6,147-6,161 vs
+// 6,090-6,110 clips/s; tools/sessions/gpu_r06p.sh).  EOSV_BNECK_TAIL (profiling build): 0 never,
+// 1 always, 2 only at W 64.
 static bool bneck_tail_eligible(const eosv_handle* h, const Block& b, const Block& nb, int hh, int ww) {
-  static const bool on = env_switch("EOSV_BNECK_TAIL", 1) != 0;
-  if (!on || !bneck_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || b.has_ds || !nb.bottleneck) return false;
+  static const int mode = env_switch("EOSV_BNECK_TAIL", 2);
+  if (!mode || (mode == 2 && ww != 64)) return false;
+  if (!bneck_enabled() || !conv_bf(h) || x3(h) || !b.bottleneck || b.has_ds || !nb.bottleneck) return false;
   const Conv &c2 = b.c2, &c3 = b.c3, &n1 = nb.c1;
   return c2.kh == 3 && c2.stride == 1 && c2.cin == 64 && c2.cout == 64 && !c2.kcm && c3.kh == 1 && c3.cin == 64 &&
          c3.cout == 256 && b.c1.cout == 64 && n1.kh == 1 && n1.stride == 1 && n1.cin == 256 && n1.cout == 128 &&
@@ -784,6 +788,55 @@ static int run_bneck_tail(eosv_handle* h, const Block& b, const Block& nb, const
   return rc;
 }
 
+// bf16 ResNet-18 stage-1 basic blocks as one launch each (bblock_bf16.hip, r06): conv1 -> conv2 + x
+// with conv1's output kept on the CU.  EOSV_BBLOCK=0 (profiling build): conv_rows_bf16 twice.
+static bool bblock_eligible(const eosv_handle* h, const Block& b, int hh, int ww) {
+#ifndef EOSV_BBLOCK_DEF
+#define EOSV_BBLOCK_DEF 1  // release A/B: tools/build_variant.sh nobb -DEOSV_BBLOCK_DEF=0
+#endif
+  static const bool on = env_switch("EOSV_BBLOCK", EOSV_BBLOCK_DEF) != 0;
+  if (!on || !conv_bf(h) || x3(h) || b.bottleneck || b.has_ds) return false;
+  const Conv &c1 = b.c1, &c2 = b.c2;
+  return c1.kh == 3 && c1.stride == 1 && c1.cin == 64 && c1.cout == 64 && !c1.kcm && c2.kh == 3 && c2.stride == 1 &&
+         c2.cin == 64 && c2.cout == 64 && !c2.kcm && bblock_bf16_ok(ww, hh);
+}
+
+static int run_bblock(eosv_handle* h, const Block& b, const void* x, void* y, int B, int hh, int ww, hipStream_t s) {
+  BneckArgs a{};
+  a.x = x;
+  a.w1 = b.c1.w;
+  a.b1 = b.c1.b;
+  a.w2 = b.c2.w;
+  a.b2 = b.c2.b;
+  a.y = y;
+  a.N = B;
+  a.H = hh;
+  a.W = ww;
+  a.cin = 64;
+  const double flops = 2.0 * B * hh * ww * 2.0 * 9 * 64 * 64;
+  if (h->planning) {
+    LaunchInfo li{};
+    a.plan = &li;
+    const int prc = launch_bblock_bf16(a, s);
+    if (prc == EOSV_OK) add_plan_cost(h, li, flops);
+    return prc;
+  }
+  poison_lds(s);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->prof) {
+    e0 = prof_event(h);
+    e1 = prof_event(h);
+    if (!e0 || !e1) return set_error("profiling: hipEventCreate failed"), EOSV_ERR_HIP;
+    EOSV_HIP_CHECK(hipEventRecord(e0, s));
+  }
+  const int rc = launch_bblock_bf16(a, s);
+  if (h->prof && rc == EOSV_OK) {
+    EOSV_HIP_CHECK(hipEventRecord(e1, s));
+    h->recs.push_back({b.c1.id, e0, e1, flops});  // profiled as the block's conv1 layer, with both convs' FLOPs
+  }
+  return rc;
+}
+
 // Residual blocks [b0, b1) on x (B frames, hh x ww) using the 4-buffer set `bufs`.  The
 // output of each block lands in place of its residual buffer; when `dst` is given, the last
 // block writes there instead (its residual still comes from `bufs`).
@@ -817,7 +870,9 @@ static int run_blocks(eosv_handle* h, size_t b0, size_t b1, void* x, void* const
       return (void*)nullptr;
     };
     const Block* nb = bi + 1 < b1 ? &h->blocks[bi + 1] : nullptr;
-    if (!b.bottleneck) {
+    if (!b.bottleneck && bblock_eligible(h, b, hh, ww)) {
+      if ((rc = run_bblock(h, b, x, y, B, hh, ww, s))) return rc;  // y = x in place, or dst
+    } else if (!b.bottleneck) {
       if ((rc = run_conv(h, b.c1, x, B, hh, ww, nullptr, fr[0], true, bf, s))) return rc;
       if ((rc = run_conv(h, b.c2, fr[0], B, ho, wo, res, y, true, bf, s, x2, hh, ww, s2))) return rc;
     } else if (!c1_done && nb && !last_in_stage(h, bi) && bneck_eligible(h, b, hh, ww)) {

@@ -175,10 +175,19 @@ def fuse_bneck_bytes(layers, spec: ResNetSpec, nl):
     folded stride-1 downsample's input: the same pixels, read once) and writes the block output; its
     64-channel maps (conv1's and conv2's outputs) never reach HBM.  Its entry moves onto conv1's id,
     with all three weight matrices; conv2 / conv3 become empty.  (A next conv1 fused into it keeps the
-    generic rule: an unlaunched conv's bytes less its input map join the previous launch.)"""
+    generic rule: an unlaunched conv's bytes less its input map join the previous launch.)
+    Basic blocks run as one launch (bblock_bf16.hip, r06: conv1 launched, conv2 not) read the
+    block input once (conv1's input is conv2's residual) and write the block output: conv2's bytes
+    less its input map, with both weight tensors."""
     L = [tuple(x) for x in layers]
     for c1, c2, c3, _ in block_layer_ids(spec):
-        if c3 is None or c3 >= len(L) or c3 >= len(nl):
+        if c3 is None:
+            if c2 < len(L) and c2 < len(nl) and nl[c1] and not nl[c2]:
+                pf2, wb2, pin2 = L[c2]
+                L[c1] = (pf2 - pin2, L[c1][1] + wb2, L[c1][2])
+                L[c2] = (0, 0, 0)
+            continue
+        if c3 >= len(L) or c3 >= len(nl):
             continue
         if nl[c1] and not nl[c2] and not nl[c3]:
             pf1, wb1, pin1 = L[c1]

@@ -471,3 +471,23 @@ def test_fused_block_bytes_follow_the_profile():
     assert F[8] == L[8] and F[9:] == L[9:]  # block 2's conv1 keeps its entry (the generic next-conv1 rule)
     # blocks run conv by conv: unchanged
     assert arch.fuse_bneck_bytes(L, spec, np.array([1 if L[i][0] else 0 for i in range(n)])) == L
+
+
+def test_fused_basic_block_bytes_follow_the_profile():
+    """r06: an R18 stage-1 basic block run as ONE launch (bblock_bf16.hip: conv1 launched, conv2 not)
+    is priced as block input + block output (conv1's input is conv2's residual, read once) with both
+    weight tensors; the conv1 output never reaches HBM."""
+    from eosv import arch
+
+    spec = arch.SPECS["resnet18"]
+    ids = arch.block_layer_ids(spec)
+    assert ids[0] == (1, 2, None, None) and ids[1] == (3, 4, None, None)
+    L = arch.conv_launch_bytes(spec, 224, 224, 2)
+    n = len(L)
+    nl = np.array([1 if L[i][0] else 0 for i in range(n)])
+    nl[[2, 4]] = 0  # both stage-1 blocks fused
+    F = arch.fuse_bneck_bytes(L, spec, nl)
+    px = 56 * 56
+    assert F[1] == (2 * px * 64 * 2, 2 * 64 * 576 * 2, px * 64 * 2) and F[3] == F[1]
+    assert F[2] == F[4] == (0, 0, 0) and F[5:] == L[5:]
+    assert arch.fuse_bneck_bytes(L, spec, np.array([1 if L[i][0] else 0 for i in range(n)])) == L

@@ -64,7 +64,16 @@ def test_bneck_bitwise_equal_unfused(name, tmp_path):
     """r06: the whole-block stage-1 kernel (bneck_bf16.hip: conv1 -> conv2 -> conv3 in one launch,
     plus the next block's conv1) against the r05 path it replaces (EOSV_BNECK=0: the 1x1 conv,
     conv_rows_bf16 / conv_rowsr_bf16 and the pair kernels): every stage map bitwise equal, at 224
-    (R50: 56x56 maps, a phantom tile per wave 3) and 256 (R101: 64x64), with one image per
+    (R50: 56x56 maps, 8 idle lanes in each row's last pixel tile) and 256 (R101: 64x64), with one image per
     workgroup (37 frames) and with 2-3 images per workgroup (601 / 300 frames on 256 CUs: the
     stream crosses images through the zero step, ragged image counts per workgroup)."""
     _switch_stage_maps_equal("EOSV_BNECK", name, tmp_path, "bneck", "r05 stage-1")
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet18:224:601", "resnet18:256", "resnet18:256:300"])
+def test_bblock_bitwise_equal_unfused(name, tmp_path):
+    """r06: the whole basic-block stage-1 kernel (bblock_bf16.hip: conv1 -> conv2 + x in one launch)
+    against the two 3x3 launches it replaces (EOSV_BBLOCK=0: conv_rows_bf16 at 56x56, the 64x64
+    kernels at 256): every stage map bitwise equal, one image per workgroup (37 frames) and several
+    (601 / 300 frames: the stream crosses images through the zero step)."""
+    _switch_stage_maps_equal("EOSV_BBLOCK", name, tmp_path, "bblock", "two-launch stage-1")
