@@ -56,9 +56,10 @@ struct BbGeo {
   static constexpr int ROWB = SLOTS * 128;   // bytes per ring row (64 bf16 per slot)
   static constexpr int XR = 8, TR = 5;       // ring rows
   static constexpr int B_OFF = 0;            // b1[64] b2[64]
+  static constexpr int PAD = 1024;            // idle lanes of the last tile read up to 8 slots past a row
   static constexpr int X_OFF = 512;
-  static constexpr int T_OFF = X_OFF + XR * ROWB;
-  static constexpr int LDS = T_OFF + TR * ROWB;
+  static constexpr int T_OFF = X_OFF + XR * ROWB + PAD;
+  static constexpr int LDS = T_OFF + TR * ROWB + PAD;
   static_assert(W > 48 && W <= 64, "four 16-column tiles per row");
   static_assert(LDS <= 163840, "LDS budget");
 };
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock_bf16_kernel(BneckArgs a) {
   // once per launch: shifts -> LDS, both rings zeroed (row -1 of the first image and every pad
   // slot), this wave's 16 couts x 576 K of both convs into registers
   for (int i = tid; i < 128; i += 64 * BB_NW) b1s[i] = i < 64 ? a.b1[i] : a.b2[i - 64];
-  for (int i = tid; i < (G::XR + G::TR) * ROWB / 16; i += 64 * BB_NW) *(v4u*)(XR + 16 * i) = v4u{0, 0, 0, 0};
+  for (int i = tid; i < (G::LDS - G::X_OFF) / 16; i += 64 * BB_NW) *(v4u*)(XR + 16 * i) = v4u{0, 0, 0, 0};
   bf16x8 w1f[18], w2f[18];
   {
     const u16* w1 = (const u16*)a.w1 + (long long)(16 * cw + r) * 576 + 8 * q;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock_bf16_kernel(BneckArgs a) {
   };
 
   // 3x3 conv of step g, step row OY, this wave's cout tile, from a ring of RING rows (stream row R
-  // at R mod RING): as conv_rows_bf16 / bneck_bf16's conv2.  Idle lanes read column W - 1.
+  // at R mod RING): as conv_rows_bf16 / bneck_bf16's conv2.
   auto conv3x3 = [&](auto second, int g, auto oyc, f32x4(&acc)[4]) {
     constexpr bool C2 = decltype(second)::value;  // conv2: T ring, w2f; conv1: X ring, w1f
     constexpr int RING = C2 ? G::TR : G::XR;
@@ -144,23 +145,36 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock_bf16_kernel(BneckArgs a) {
     int rowb[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) rowb[j] = __builtin_amdgcn_readfirstlane(((2 * g + OY + j - 1 + RING) % RING) * ROWB);
-    int cq[4][3];
+    // lane (q, r) of tile u reads slot 16u + r + dx, chunk q (^ 4 for the second half) swizzled by
+    // the slot: (16u + r + dx) & 7 = (r + dx) & 7, so the per-lane part is one offset per dx and the
+    // tile is a compile-time 2048 u.  Idle lanes (16u + r >= W) read past their row: ring pad.
+    int e[3];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = 16 * u + r < W ? 16 * u + r : W - 1;
+    for (int dx = 0; dx < 3; ++dx) e[dx] = (r + dx) * 128 + ((q ^ ((r + dx) & 7)) << 4);
+    auto rd = [&](int t2, bf16x8(&bf)[4]) __attribute__((always_inline)) {
+      const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+      const unsigned char* base = ring + rowb[dy] + ((t2 & 1) ? (e[dx] ^ 64) : e[dx]);
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) cq[u][dx] = (c + dx) * 128 + ((q ^ ((c + dx) & 7)) << 4);
-    }
+      for (int u = 0; u < 4; ++u) bf[u] = *(const bf16x8*)(base + 2048 * u);
+    };
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // B fragments double-buffered (as conv_rows_bf16): step t2 + 1's reads go out before step t2's
+    // MFMAs, one lgkmcnt(0) after them
+    bf16x8 bf[2][4];
+    rd(0, bf[0]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t2 = 0; t2 < 18; ++t2) {
-      const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
-      bf16x8 bf[4];
+      if (t2 + 1 < 18) rd(t2 + 1, bf[(t2 + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) bf[u] = *(const bf16x8*)(ring + rowb[dy] + ((t2 & 1) ? (cq[u][dx] ^ 64) : cq[u][dx]));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(C2 ? w2f[t2] : w1f[t2], bf[u], acc[u], 0, 0, 0);
+      for (int u = 0; u < 4; ++u)
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(C2 ? w2f[t2] : w1f[t2], bf[t2 & 1][u], acc[u], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 

@@ -63,6 +63,43 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long lo
 }
 }  // namespace
 
+// conv2: 18 k-steps (tap-major, two 32-channel halves per tap) of one 16-cout tile over the four
+// 16-pixel tiles of a step row, B fragments from the T1 ring (rowb: the three input rows' byte
+// offsets).  Lane (q, r) of tile u reads slot 16u + r + dx, chunk q (^ 4 for the second half),
+// swizzled by the slot: (16u + r + dx) & 7 = (r + dx) & 7, so the per-lane part is one offset per dx
+// and the tile a compile-time 2048 u (idle lanes of W 56 read past their row: the next ring row or
+// T2, harmless).  Fragments double-buffered: step t + 1's reads go out before step t's MFMAs, one
+// lgkmcnt(0) after them (as conv_rows_bf16).
+__device__ __forceinline__ void conv2_ring(const unsigned char* T1, const int (&rowb)[3], int r, int q,
+                                           const bf16x8 (&wf)[18], f32x4 (&acc)[4], bool skip) {
+  int e[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) e[dx] = (r + dx) * 128 + ((q ^ ((r + dx) & 7)) << 4);
+  auto rd = [&](int t2, bf16x8(&bf)[4]) __attribute__((always_inline)) {
+    const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+    const unsigned char* base = T1 + rowb[dy] + ((t2 & 1) ? (e[dx] ^ 64) : e[dx]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bf[u] = *(const bf16x8*)(base + 2048 * u);
+  };
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (skip) return;
+  bf16x8 bf[2][4];
+  rd(0, bf[0]);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t2 = 0; t2 < 18; ++t2) {
+    if (t2 + 1 < 18) rd(t2 + 1, bf[(t2 + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t2], bf[t2 & 1][u], acc[u], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 constexpr int BN_NW = 8;  // waves per workgroup (two per SIMD; <= 256 VGPRs each)
 
 // Geometry of a step (two image rows): pixel tile t (0..7) is row t >> 2, columns 16 (t & 3) ..
@@ -240,28 +277,8 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_bf16_kernel(BneckArgs a) {
     int rowb[3];  // byte offsets of T1 ring rows 2g + OY - 1 .. + 1 (wave-uniform)
 #pragma unroll
     for (int j = 0; j < 3; ++j) rowb[j] = __builtin_amdgcn_readfirstlane(((2 * g + OY + j + 4) % 5) * ROWB);
-    // per tile u (columns 16u + r) and tap column dx: the lane's slot and swizzled chunk for k-slice
-    // half 0 (half 1 is chunk ^ 4, i.e. the byte offset ^ 64)
-    int cq[4][3];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = 16 * u + r < W ? 16 * u + r : W - 1;
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) cq[u][dx] = (c + dx) * 128 + ((q ^ ((c + dx) & 7)) << 4);
-    }
     f32x4 acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t2 = 0; t2 < 18; ++t2) {
-      if (abl & 2) break;
-      const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
-      bf16x8 bf[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) bf[u] = *(const bf16x8*)(T1 + rowb[dy] + ((t2 & 1) ? (cq[u][dx] ^ 64) : cq[u][dx]));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[t2], bf[u], acc[u], 0, 0, 0);
-    }
+    conv2_ring(T1, rowb, r, q, w2f, acc, abl & 2);
     // epilogue: couts 16 cw + 4q .. + 3 of column 16u + r: + shift, ReLU, bf16 -> T2 (8 B, chunk
     // 2 cw + q / 2 of the pixel's 8, swizzled by the pixel)
     const f32x4 bias = *(const f32x4*)(b2s + 16 * cw + 4 * q);
@@ -522,25 +539,8 @@ __global__ __launch_bounds__(64 * BN_NW) void bneck_tail_bf16_kernel(BneckArgs a
     int rowb[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) rowb[j] = __builtin_amdgcn_readfirstlane(((2 * g + OY + j + 4) % 5) * ROWB);
-    int cq[4][3];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = 16 * u + r < W ? 16 * u + r : W - 1;
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) cq[u][dx] = (c + dx) * 128 + ((q ^ ((c + dx) & 7)) << 4);
-    }
     f32x4 acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t2 = 0; t2 < 18; ++t2) {
-      const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
-      bf16x8 bf[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) bf[u] = *(const bf16x8*)(T1 + rowb[dy] + ((t2 & 1) ? (cq[u][dx] ^ 64) : cq[u][dx]));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[t2], bf[u], acc[u], 0, 0, 0);
-    }
+    conv2_ring(T1, rowb, r, q, w2f, acc, false);
     const f32x4 bias = *(const f32x4*)(b2s + 16 * cw + 4 * q);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
