@@ -1,4 +1,4 @@
-// Layer-level check of bneck_bf16 (the r06 whole-block stage-1 kernel) and bneck_tail_bf16: seeded
+// Layer-level check of bneck_bf16 (the r06 whole-block stage-1 kernel), bneck_tail_bf16 and bblock_bf16: seeded
 // random bf16 operands, every output checked against a CPU reference (f32 accumulation, bf16 rounding
 // between the convs as the kernels do; tolerance for the summation order), and REPEAT launches on
 // the same inputs compared bitwise -- a race shows as run-to-run differences, reported with its
@@ -185,6 +185,92 @@ static int check(int N, int H, int W, int cin, bool next, bool tail, int reps) {
   return bad || racy ? 1 : 0;
 }
 
+// bblock_bf16 (the fused R18 stage-1 basic block): y = relu(conv2(relu(conv1(x) + b1)) + b2 + x),
+// checked like the bottleneck kernels (CPU reference over the first images + repeat launches), in
+// place (y = x, as the engine runs it) when inplace is set
+static int check_bblock(int N, int H, int W, bool inplace, int reps) {
+  unsigned s = 4242u + 17u * (unsigned)(N * 7 + H + inplace);
+  const int M = N * H * W;
+  std::vector<u16> x((size_t)M * 64), w1((size_t)64 * 576), w2((size_t)64 * 576);
+  std::vector<float> b1(64), b2(64);
+  for (auto& e : x) e = f2bf(frand(s));
+  for (auto& e : w1) e = f2bf(frand(s) * 0.05f);
+  for (auto& e : w2) e = f2bf(frand(s) * 0.05f);
+  for (auto& e : b1) e = frand(s) * 0.1f;
+  for (auto& e : b2) e = frand(s) * 0.1f;
+  const int NR = N < 3 ? N : 3;
+  auto conv = [&](const std::vector<float>& in, const std::vector<u16>& w, std::vector<float>& out) {
+    for (int n = 0; n < NR; ++n)
+      for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j)
+          for (int o = 0; o < 64; ++o) {
+            float a = 0.f;
+            for (int dy = 0; dy < 3; ++dy)
+              for (int dx = 0; dx < 3; ++dx) {
+                const int ii = i + dy - 1, jj = j + dx - 1;
+                if (ii < 0 || ii >= H || jj < 0 || jj >= W) continue;
+                const float* tp = &in[(((size_t)n * H + ii) * W + jj) * 64];
+                const u16* wp = &w[(size_t)o * 576 + (dy * 3 + dx) * 64];
+                for (int c = 0; c < 64; ++c) a += bf2f(wp[c]) * tp[c];
+              }
+            out[(((size_t)n * H + i) * W + j) * 64 + o] = a;
+          }
+  };
+  const size_t MR = (size_t)NR * H * W;
+  std::vector<float> xf(MR * 64), t(MR * 64), y(MR * 64);
+  for (size_t i = 0; i < MR * 64; ++i) xf[i] = bf2f(x[i]);
+  conv(xf, w1, t);
+  for (size_t i = 0; i < MR * 64; ++i) t[i] = rb(fmaxf(t[i] + b1[i % 64], 0.f));
+  conv(t, w2, y);
+  for (size_t i = 0; i < MR * 64; ++i) y[i] = rb(fmaxf(y[i] + b2[i % 64] + xf[i], 0.f));
+  Dev dx(x.size() * 2), dy(x.size() * 2), dw1(w1.size() * 2), dw2(w2.size() * 2), db1(256), db2(256);
+  up(dw1, w1);
+  up(dw2, w2);
+  up(db1, b1);
+  up(db2, b2);
+  BneckArgs a{};
+  a.x = dx.p;
+  a.w1 = dw1.p;
+  a.b1 = (const float*)db1.p;
+  a.w2 = dw2.p;
+  a.b2 = (const float*)db2.p;
+  a.y = inplace ? dx.p : dy.p;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.cin = 64;
+  std::vector<u16> y0(x.size()), y1(x.size());
+  int bad = 0, racy = 0;
+  double maxerr = 0.0;
+  for (int rep = 0; rep < reps; ++rep) {
+    up(dx, x);  // in place overwrites the input: restore it every launch
+    if (!inplace) hipMemset(dy.p, 0xff, x.size() * 2);
+    if (launch_bblock_bf16(a, nullptr) || hipDeviceSynchronize() != hipSuccess) {
+      printf("FAIL launch %s\n", eosv_last_error());
+      return 1;
+    }
+    hipMemcpy(rep ? y1.data() : y0.data(), a.y, x.size() * 2, hipMemcpyDeviceToHost);
+    if (rep)
+      for (size_t i = 0; i < y0.size(); ++i)
+        if (y0[i] != y1[i] && racy++ < 4) {
+          const size_t p = i / 64;
+          printf("  race Y rep %d: image %zu row %zu col %zu ch %zu\n", rep, p / (H * W), (p / W) % H, p % W, i % 64);
+        }
+  }
+  for (size_t i = 0; i < MR * 64; ++i) {
+    const double e = fabs((double)bf2f(y0[i]) - y[i]);
+    maxerr = fmax(maxerr, e);
+    if (e > 0.05 + 0.02 * fabs(y[i]) && bad++ < 4) {
+      const size_t p = i / 64;
+      printf("  bad Y image %zu row %zu col %zu ch %zu: got %g ref %g\n", p / (H * W), (p / W) % H, p % W, i % 64,
+             bf2f(y0[i]), y[i]);
+    }
+  }
+  printf("%s bblock N%d H%d W%d %s reps %d: maxerr %.3g bad %d racy %d\n", bad || racy ? "FAIL" : "ok  ", N, H, W,
+         inplace ? "in place" : "out of place", reps, maxerr, bad, racy);
+  return bad || racy ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 4;
   int fails = 0;
@@ -197,6 +283,10 @@ int main(int argc, char** argv) {
     fails += check(300, W, W, 64, false, false, 2);
     fails += check(300, W, W, 256, true, false, 2);
     fails += check(300, W, W, 64, false, true, 2);
+  }
+  for (int W : {56, 64}) {
+    fails += check_bblock(37, W, W, true, reps);
+    fails += check_bblock(300, W, W, false, 2);
   }
   printf("\n%d failures\n", fails);
   return fails ? 1 : 0;
