@@ -275,13 +275,270 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock_bf16_kernel(BneckArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the last stores (and empty prefetches) have left
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-conv form (r06, bblock2): the same stream of two-row steps, but each wave runs ONE of the
+// two convs for 32 couts (two 16-cout tiles) of one step row: waves 0-3 conv1, waves 4-7 conv2
+// (a workgroup's waves fill the SIMDs cyclically, so every SIMD holds one of each).  Why: in
+// bblock_bf16_kernel every wave reads each B fragment for ONE 16-cout tile, so per step the CU
+// reads 1152 KiB of fragments from LDS -- 4608 LDS cycles at 256 B/clk, exactly the 4608 MFMA
+// cycles per SIMD: the kernel is co-bound by the LDS and the MFMA pipe (MFMA-busy 0.54).  Here a
+// fragment feeds two MFMAs (576 KiB per step), the weights of one conv (2 x 18 fragments, 144
+// VGPRs) fit where both convs' 16-cout halves did, and the two convs run in the same phase on
+// different steps, so one barrier per step instead of two:
+//   phase g:  X rows of step g + 3 -> X ring (10 rows), step g + 4's loads go out
+//             conv1 waves: conv1 of step g + 1 (X rows 2g + 1 .. 2g + 4) -> T ring (7 rows)
+//             conv2 waves: conv2 of step g - 1 (T rows 2g - 3 .. 2g) + residual (X ring) -> y
+//             | barrier |
+// Ring rows written in phase g (X 2g + 6, 2g + 7; T 2g + 2, 2g + 3) take the slots of rows last
+// read in phase g - 1.  Per accumulator the MFMAs are those of bblock_bf16_kernel in the same K
+// order, and the epilogues are the same: bitwise equal.
+template <int W>
+struct Bb2Geo {
+  static constexpr int SP = 2 * W;
+  // ring rows of 66 slots at W 56 too: the idle lanes of the last pixel tile (columns W .. 63)
+  // write zeros into slots W + 1 .. 64 (the right pad slot W + 1 must stay zero, and does), so no
+  // lane needs its own branch or address clamp
+  static constexpr int SLOTS = 66;
+  static constexpr int ROWB = SLOTS * 128;
+  static constexpr int XR = 10, TR = 7;      // ring rows
+  static constexpr int PAD = 1024;
+  static constexpr int X_OFF = 512;          // b1[64] b2[64] before it
+  static constexpr int T_OFF = X_OFF + XR * ROWB + PAD;
+  static constexpr int LDS = T_OFF + TR * ROWB + PAD;
+  static_assert(W > 48 && W <= 64, "four 16-column tiles per row");
+  static_assert(LDS <= 163840, "LDS budget");
+};
+
+template <int W>
+__global__ __launch_bounds__(64 * BB_NW) void bblock2_bf16_kernel(BneckArgs a) {
+  using G = Bb2Geo<W>;
+  constexpr int SP = G::SP, ROWB = G::ROWB, XRN = G::XR, TRN = G::TR;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS];
+  float* const b1s = (float*)smem;
+  float* const b2s = b1s + 64;
+  unsigned char* const XR = smem + G::X_OFF;
+  unsigned char* const TRg = smem + G::T_OFF;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const int grp = w >> 2;         // 0: conv1 waves, 1: conv2 waves
+  const int cy = (w >> 1) & 1;    // the conv's step row
+  const int ch = w & 1;           // its cout half: tiles 2 ch, 2 ch + 1 (couts 32 ch ..)
+  // loads (every wave, as bblock_bf16_kernel): pixel tile w & 3 of step row w >> 2
+  const int oy = w >> 2, ox = 16 * (w & 3) + r;
+  const int poff = ox < W ? oy * W + ox : SP;  // idle lanes: pixel SP, past every step resource
+  const int H = a.H;
+  const int NS = H / 2 + 1;
+  const int GR = gridDim.x;
+  const int nimg = (a.N - (int)blockIdx.x + GR - 1) / GR;
+  const int total = nimg * NS;
+  auto is_zero = [&](int g) { return g % NS == NS - 1; };
+  auto step_res = [&](const void* base, int g) {
+    const int img = (int)blockIdx.x + (g / NS) * GR;
+    const int k = g - (g / NS) * NS;
+    const long long p0 = ((long long)img * H + 2 * k) * W;
+    return bb_rsrc((const u16*)base + p0 * 64, g >= 0 && g < total && k < NS - 1 ? (long long)SP * 128 : 0);
+  };
+
+  for (int i = tid; i < 128; i += 64 * BB_NW) b1s[i] = i < 64 ? a.b1[i] : a.b2[i - 64];
+  for (int i = tid; i < (G::LDS - G::X_OFF) / 16; i += 64 * BB_NW) *(v4u*)(XR + 16 * i) = v4u{0, 0, 0, 0};
+  // this wave's conv: 32 couts x 576 K (tile t: couts 16 (2 ch + t) + r)
+  bf16x8 wf[2][18];
+  {
+    const u16* wsrc = (const u16*)(grp ? a.w2 : a.w1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const u16* wr = wsrc + (long long)(16 * (2 * ch + t) + r) * 576 + 8 * q;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) wf[t][k] = *(const bf16x8*)(wr + (k >> 1) * 64 + 32 * (k & 1));
+    }
+  }
+
+  typedef v4u XSet[2];
+  auto load_x = [&](int g, XSet& X) {
+    const __amdgpu_buffer_rsrc_t rx = step_res(a.x, g);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) X[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, (poff * 64 + 8 * q) * 2, 64 * s, 0);
+  };
+  const int xlo = (ox + 1) * 128 + ((q ^ ((ox + 1) & 7)) << 4);
+  auto put_x = [&](int g, const XSet& X) __attribute__((always_inline)) {
+    if (is_zero(g)) {
+      for (int i = tid; i < 2 * W * 8; i += 64 * BB_NW) {
+        const int ry = i >= W * 8 ? 1 : 0, j = i - ry * W * 8;
+        *(v4u*)(XR + ((2 * g + ry) % XRN) * ROWB + 128 + 16 * j) = v4u{0, 0, 0, 0};
+      }
+      return;
+    }
+    {  // idle lanes (ox >= W) loaded zeros past the step resource and write them.  The row base
+      // is scalar, the lane part one VGPR (chunk 4 + q of the slot is chunk q's address ^ 64)
+      const int rb = __builtin_amdgcn_readfirstlane(((2 * g + oy) % XRN) * ROWB);
+      *(v4u*)(XR + rb + xlo) = X[0];
+      *(v4u*)(XR + rb + (xlo ^ 64)) = X[1];
+    }
+  };
+
+  // 3x3 conv of step g, step row OY, this wave's two cout tiles: acc[t][u] (tile t, pixel tile u)
+  auto conv3x3 = [&](auto second, int g, f32x4(&acc)[2][4]) {
+    constexpr bool C2 = decltype(second)::value;
+    constexpr int RING = C2 ? TRN : XRN;
+    const int OY = cy;
+    const unsigned char* ring = C2 ? TRg : XR;
+    int rowb[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) rowb[j] = __builtin_amdgcn_readfirstlane(((2 * g + OY + j - 1 + 2 * RING) % RING) * ROWB);
+    int e[3];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) e[dx] = (r + dx) * 128 + ((q ^ ((r + dx) & 7)) << 4);
+    auto rd = [&](int t2, bf16x8(&bf)[4]) __attribute__((always_inline)) {
+      const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+      const unsigned char* base = ring + rowb[dy] + ((t2 & 1) ? (e[dx] ^ 64) : e[dx]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bf[u] = *(const bf16x8*)(base + 2048 * u);
+    };
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 bf[2][4];
+    rd(0, bf[0]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t2 = 0; t2 < 18; ++t2) {
+      if (t2 + 1 < 18) rd(t2 + 1, bf[(t2 + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][t2], bf[t2 & 1][u], acc[t][u], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // conv1 of step g -> T ring rows 2g, 2g + 1 (% 7); a zero step writes zero rows (conv1 waves)
+  auto conv1 = [&](int g) __attribute__((always_inline)) {
+    if (is_zero(g)) {
+      for (int i = tid; i < 2 * W * 8; i += 64 * 4) {
+        const int ry = i >= W * 8 ? 1 : 0, j = i - ry * W * 8;
+        *(v4u*)(TRg + ((2 * g + ry) % TRN) * ROWB + 128 + 16 * j) = v4u{0, 0, 0, 0};
+      }
+      return;
+    }
+    f32x4 acc[2][4];
+    conv3x3(std::false_type{}, g, acc);
+    unsigned char* trow = TRg + ((2 * g + cy) % TRN) * ROWB;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int cw = 2 * ch + t;
+      const f32x4 bias = *(const f32x4*)(b1s + 16 * cw + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int s = 16 * u + r + 1;
+        uint2 pk = make_uint2(relu_bf2(acc[t][u].lo + bias.lo), relu_bf2(acc[t][u].hi + bias.hi));
+        if (16 * u + r >= W) pk = make_uint2(0u, 0u);  // idle column: a zero slot
+        *(uint2*)(trow + s * 128 + (((2 * cw + (q >> 1)) ^ (s & 7)) << 4) + 8 * (q & 1)) = pk;
+      }
+    }
+  };
+  // conv2 of step g + the residual (X ring rows 2g, 2g + 1): the 8 packed results and their store
+  // offsets (idle lanes: offsets past the step resource); the stores themselves are common code
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  auto conv2 = [&](int g, u32x2(&spk)[8], int(&svo)[8]) __attribute__((always_inline)) {
+    f32x4 acc[2][4];
+    conv3x3(std::true_type{}, g, acc);
+    const unsigned char* xrow = XR + ((2 * g + cy + XRN) % XRN) * ROWB;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int cw = 2 * ch + t;
+      const f32x4 bias = *(const f32x4*)(b2s + 16 * cw + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int col = 16 * u + r;
+        const int s = col + 1;  // (idle columns: a zero slot, their store is dropped)
+        const uint2 rv = *(const uint2*)(xrow + s * 128 + (((2 * cw + (q >> 1)) ^ (s & 7)) << 4) + 8 * (q & 1));
+        spk[4 * t + u] = u32x2{relu_bf2(acc[t][u].lo + bias.lo + bf2_f(rv.x)),
+                               relu_bf2(acc[t][u].hi + bias.hi + bf2_f(rv.y))};
+        const int p = col < W ? cy * W + col : SP;
+        svo[4 * t + u] = (p * 64 + 16 * cw + 4 * q) * 2;
+      }
+    }
+  };
+
+  auto lds_barrier = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: steps 0-2 in the ring, step 3 in flight, conv1 of step 0.  One register set for the
+  // X loads: a phase puts the set it waited for, then reloads it (the ring writes read their data at
+  // issue, before any load can return into it)
+  XSet S;
+  load_x(0, S);
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): weights, shifts, step 0's rows
+  __syncthreads();                     // rings zeroed, shifts visible
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    if (g) __builtin_amdgcn_s_waitcnt(0x0f70);
+    put_x(g, S);
+    load_x(g + 1, S);
+  }
+  lds_barrier();
+  if (grp == 0) conv1(0);
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): X(3) too (phase 0's counted wait sees no stores before it)
+  lds_barrier();
+  // phase g: X(g + 3) (loaded in phase g - 1) -> ring, X(g + 4) into the same registers, then
+  // conv1 of step g + 1 or conv2 of step g - 1.  VMEM per wave and phase in issue order: 2 loads,
+  // then (conv2 waves) 8 stores -- also in phase 0, whose conv2 of step -1 stores into an empty
+  // resource -- so the counted wait below is the only one.
+  // Both groups issue the same 8 stores after the branch (the conv1 waves' into an empty resource,
+  // dropped without memory traffic): one VMEM sequence per phase on every path, so hipcc's own wait
+  // before the ring writes is the counted vmcnt(8) -- stores inside the conv2 branch gave it a path
+  // without them, and a vmcnt(0) at the top of every phase (as bblock_bf16_kernel's note says)
+  const __amdgpu_buffer_rsrc_t nowhere = bb_rsrc(a.y, 0);
+  for (int g = 0; g <= total; ++g) {
+    vm_wait<8>();  // S has landed: younger are only the previous phase's stores
+    put_x(g + 3, S);
+    load_x(g + 4, S);
+    u32x2 spk[8];
+    int svo[8];
+    __amdgpu_buffer_rsrc_t srs = nowhere;
+    if (grp == 0) {
+      if (g + 1 < total) conv1(g + 1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) spk[k] = u32x2{0u, 0u}, svo[k] = 16 * k;
+    } else {
+      conv2(g - 1, spk, svo);
+      srs = step_res(a.y, g - 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b64(spk[k], srs, svo[k], 0, 0);
+    lds_barrier();
+  }
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the last stores (and empty prefetches) have left
+}
+
 bool bblock_bf16_ok(int W, int H) { return (W == 56 || W == 64) && H >= 2 && H % 2 == 0; }
+
+#ifndef EOSV_BBLOCK2_DEF
+#define EOSV_BBLOCK2_DEF 1
+#endif
 
 template <int W>
 static int launch_bb(const BneckArgs& a, hipStream_t s) {
   if (a.plan) return record_launch(a.plan, a.N, 1);
   const int grid = std::min(a.N, device_cu_count());
-  hipLaunchKernelGGL((bblock_bf16_kernel<W>), dim3(grid), dim3(64 * BB_NW), 0, s, a);
+  static const int v2 = env_switch("EOSV_BBLOCK2", EOSV_BBLOCK2_DEF);  // 0: the r06 one-wave-both-convs kernel (A/B)
+  if (v2)
+    hipLaunchKernelGGL((bblock2_bf16_kernel<W>), dim3(grid), dim3(64 * BB_NW), 0, s, a);
+  else
+    hipLaunchKernelGGL((bblock_bf16_kernel<W>), dim3(grid), dim3(64 * BB_NW), 0, s, a);
   EOSV_LAUNCH_CHECK();
   return EOSV_OK;
 }

@@ -512,6 +512,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_kernel(ConvArgs a) {
 // ahead) and 2 B slots (the weights, one ahead), 160 KiB (256x256 tiles; r04 A/B on the stride-1
 // 3x3s: one ring 6-7 %, split rings 13 % faster than conv_bf16_kernel's one ring).  DS / SPLIT as in
 // conv_bf16_kernel (the folded downsample's K columns; the f32x3 split layout).
+#ifndef EOSV_BF16_WS_BEARLY
+#define EOSV_BF16_WS_BEARLY 1
+#endif
 template <int BM, int BN, int WM, int WN, int NP, int NSA, bool DS, bool SPLIT>
 __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvArgs a) {
   constexpr int BK = 64, CPR = 8, RPP = 8, MF = 16, KS = 32;
@@ -680,7 +683,26 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         const int i = g - (g / TM) * TM;
-        if (g > 0 && g % TM == 0) rdB(g / TM);  // slice boundary: this slice's B (not overlapped)
+        if constexpr (EOSV_BF16_WS_BEARLY) {
+          if (g % TM == TM - 1 && g + 1 < NG) {
+            // a slice's last group: B fragment j of the next slice is read right behind the MFMA
+            // that last uses fragment j of this slice (the slice-boundary read then has three
+            // MFMAs of lead instead of none)
+            afr[(g + 1) & 1] = rdA(g + 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[g & 1], bfr[j], acc[i][j], 0, 0, 0);
+              const int s1 = g / TM + 1;
+              bfr[j] = *(const bf16x8*)(Bs + (wn * (BN / WN) + j * MF + r) * BK + ((s1 * (KS / 8) + q) ^ sw) * 8);
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+          }
+        }
+        if (!EOSV_BF16_WS_BEARLY && g > 0 && g % TM == 0) rdB(g / TM);  // slice boundary: this slice's B (not overlapped)
         if (g + 1 < NG) afr[(g + 1) & 1] = rdA(g + 1);
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (g + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);

@@ -322,6 +322,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_bf16_ts_kernel(ConvArgs a) 
 // rings: 3 A slots (the stage's input row, two stages ahead) and 2 B slots (its 3 taps' weights,
 // one ahead), 147 KiB at 512 x 128.  Same stages, taps, MFMA order and epilogue as
 // conv_bf16_ts_kernel: bit-identical outputs.
+#ifndef EOSV_BF16_TS_BEARLY
+#define EOSV_BF16_TS_BEARLY 1
+#endif
 template <int BM, int BN, int WM, int WN, int NP>
 __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(ConvArgs a) {
   constexpr int BK = 32, NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
@@ -475,6 +478,49 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(Co
     const u16* As = a_slot(st);
     const u16* Bs = b_slot(st);
     const bool ds = st >= nst3;  // a DS stage is read at offset 1 only (no taps, no edges)
+#if EOSV_BF16_TS_BEARLY
+    // BEARLY (r06 A/B): taps 1 and 2 of a 3x3 stage get their B fragments and first A fragment in
+    // the previous tap's last group, fragment j right behind the MFMA that last reads the previous
+    // tap's fragment j.  A DS stage runs its one tap (offset 1) as iteration 0, so the reads at an
+    // iteration's start stay unconditional (a runtime branch around them spilled the tile)
+    bf16x8 bfr[TN], afr[2];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      if (ds && kw != 0) continue;
+      const int tap = ds ? 1 : kw;
+      auto rdB = [&](int tp, int j) {
+        const int row = tp * BN + wn * (BN / WN) + j * 16 + r;
+        return *(const bf16x8*)(Bs + row * BK + ((q ^ ((row >> 1) & 3)) * 8));
+      };
+      auto rdAt = [&](int tp, int i) {
+        const int row = wm * (BM / WM) + i * 16 + r + tp;  // pixel m0 + (row - tp) at tap tp
+        bf16x8 f = *(const bf16x8*)(As + row * BK + ((q ^ ((row >> 1) & 3)) * 8));
+        if (tp != 1 && ((emask >> (2 * i + (tp >> 1))) & 1)) f = bf16x8{};
+        return f;
+      };
+      auto rdA = [&](int i) { return rdAt(tap, i); };
+      if (kw == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = rdB(tap, j);
+        afr[0] = rdA(0);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (kw < 2 && i == TM - 1) {  // (a DS stage reads tap 1's fragments here and never uses them)
+          static_assert(TM % 2 == 0, "the next tap's first A fragment goes into the free slot 0");
+          afr[0] = rdAt(kw + 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[j], acc[i][j], 0, 0, 0);
+            bfr[j] = rdB(kw + 1, j);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
+        }
+#else
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       if (ds && kw != 1) continue;
@@ -493,6 +539,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(Co
       afr[0] = rdA(0);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
+#endif
         if (i + 1 < TM) afr[(i + 1) & 1] = rdA(i + 1);
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (i + 1 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);

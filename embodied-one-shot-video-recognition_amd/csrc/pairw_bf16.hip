@@ -95,9 +95,13 @@ struct PairW {
 // ops (vmcnt retires loads, stores and LDS-DMA together in issue order, MI355X_MICROARCH.md), so
 // they do not drain the residual prefetch; without CS they count loads only (r03), which is
 // stricter whenever a store is still in flight.
+#ifndef EOSV_PAIRW_FD
+#define EOSV_PAIRW_FD 2
+#endif
 template <int CMID, int CEXP, int C1, int NPT, int DSC, bool CS, bool ABL = false>
 __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
   using P = PairW<CMID, CEXP, C1, NPT, DSC>;
+  constexpr int FD = NPT == 1 ? EOSV_PAIRW_FD : 2;
   const int abl = ABL ? a.abl : 0;
   constexpr int K3 = P::K3, XSM = P::XSM;
   constexpr int NCH = P::NCH, XS = P::XS, G2 = P::G2, PPW = P::PPW, NT = 64 * P::NW;
@@ -307,8 +311,10 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
           }
         }
       };
-      bf16x8 fr[2][4];
+      // FD fragment groups in flight (r06: FD 3 = two groups read ahead where the registers allow)
+      bf16x8 fr[FD][4];
       frags(0, fr[0]);
+      if constexpr (FD == 3) frags(1, fr[1]);
       f32x4 acc1[NPT][4];
 #pragma unroll
       for (int t = 0; t < NPT; ++t)
@@ -325,9 +331,9 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
           load_r(rr, here ? ch + RD : ch + RD - NCH, rres[(u + RD) & 3]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (gi + 1 < NG) frags(gi + 1, fr[(gi + 1) & 1]);
-        // the next group's 4 LDS reads issue before this group's 4 MFMAs
-        if (gi + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        if (gi + FD - 1 < NG) frags(gi + FD - 1, fr[(gi + FD - 1) % FD]);
+        // the next group's (FD 3: the one after next) 4 LDS reads issue before this group's 4 MFMAs
+        if (gi + FD - 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 4 * NPT, 0);
         if (abl & 8) {
         } else if (gi < XS) {  // GEMM1: chunk couts, tiles i = 0..3 of 16 permuted rows
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
             const bf16x8 bx = __builtin_bit_cast(bf16x8, xf[t][gi]);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              acc1[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], bx, acc1[t][i], 0, 0, 0);
+              acc1[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi % FD][i], bx, acc1[t][i], 0, 0, 0);
           }
         } else {  // GEMM2: D2[64g + permuted rows][px] += W1[.., k-slice s2 of the chunk] . Ychunk
           const int s2 = (gi - XS) / G2, g = (gi - XS) % G2;
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(512, 1) void pairw_bf16_kernel(Pair1x1Args a) {
           for (int t = 0; t < NPT; ++t)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              acc2[t][g][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi & 1][i], yf[t][s2], acc2[t][g][i], 0, 0, 0);
+              acc2[t][g][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[gi % FD][i], yf[t][s2], acc2[t][g][i], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (gi == XS - 1) {
