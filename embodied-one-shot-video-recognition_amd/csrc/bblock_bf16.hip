@@ -309,6 +309,14 @@ struct Bb2Geo {
   static_assert(LDS <= 163840, "LDS budget");
 };
 
+// timing-only ablations of release variants (results wrong): 1 no MFMAs, 2 no fragment reads after
+// the first, 4 no phase barriers
+#ifndef EOSV_BB2_LEAD
+#define EOSV_BB2_LEAD 1
+#endif
+#ifndef EOSV_BB2_ABL
+#define EOSV_BB2_ABL 0
+#endif
 template <int W>
 __global__ __launch_bounds__(64 * BB_NW) void bblock2_bf16_kernel(BneckArgs a) {
   using G = Bb2Geo<W>;
@@ -373,9 +381,9 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock2_bf16_kernel(BneckArgs a) {
     }
     {  // idle lanes (ox >= W) loaded zeros past the step resource and write them.  The row base
       // is scalar, the lane part one VGPR (chunk 4 + q of the slot is chunk q's address ^ 64)
-      const int rb = __builtin_amdgcn_readfirstlane(((2 * g + oy) % XRN) * ROWB);
-      *(v4u*)(XR + rb + xlo) = X[0];
-      *(v4u*)(XR + rb + (xlo ^ 64)) = X[1];
+      const int o0 = __builtin_amdgcn_readfirstlane(((2 * g + oy) % XRN) * ROWB) + xlo;
+      *(v4u*)(XR + o0) = X[0];
+      *(v4u*)(XR + (o0 ^ 64)) = X[1];  // (XR and the rows are 128-B aligned)
     }
   };
 
@@ -402,17 +410,50 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock2_bf16_kernel(BneckArgs a) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x8 bf[2][4];
+#if EOSV_BB2_LEAD
+    // Fragment (t2 + 2, u) is read into the slot of (t2, u) right behind the two MFMAs that last read
+    // it: every read has ~1.75 k-steps (7 reads) of lead, in the same 8 fragment registers, and hipcc
+    // waits lgkmcnt(7) per pixel tile instead of lgkmcnt(0) per k-step (the skeleton of LDS latency
+    // waits, 0.87 of the 1.42 ms per launch without MFMAs, no longer runs beside them but under them)
+    auto rd1 = [&](int t2, int u) __attribute__((always_inline)) {
+      const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+      // the second channel half is the first's address ^ 64 (ring rows are 128-B aligned)
+      const int a0 = rowb[dy] + e[dx];
+      return *(const bf16x8*)(ring + ((t2 & 1) ? (a0 ^ 64) : a0) + 2048 * u);
+    };
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bf[0][u] = rd1(0, u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bf[1][u] = rd1(1, u);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t2 = 0; t2 < 18; ++t2) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          if constexpr (EOSV_BB2_ABL & 1) asm volatile("" ::"v"(bf[t2 & 1][u])); else  // (timing ablation)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][t2], bf[t2 & 1][u], acc[t][u], 0, 0, 0);
+        if (t2 + 2 < 18) bf[t2 & 1][u] = rd1(t2 + 2, u);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (t2 + 2 < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return;
+#endif
     rd(0, bf[0]);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t2 = 0; t2 < 18; ++t2) {
-      if (t2 + 1 < 18) rd(t2 + 1, bf[(t2 + 1) & 1]);
+      if (t2 + 1 < 18 && !(EOSV_BB2_ABL & 2)) rd(t2 + 1, bf[(t2 + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
+          if constexpr (EOSV_BB2_ABL & 1) asm volatile("" ::"v"(bf[t2 & 1][u])); else  // (timing ablation)
           acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][t2], bf[t2 & 1][u], acc[t][u], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -519,7 +560,7 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock2_bf16_kernel(BneckArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b64(spk[k], srs, svo[k], 0, 0);
-    lds_barrier();
+    if (!(EOSV_BB2_ABL & 4)) lds_barrier();
   }
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the last stores (and empty prefetches) have left
 }

@@ -70,6 +70,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long lo
 // and the tile a compile-time 2048 u (idle lanes of W 56 read past their row: the next ring row or
 // T2, harmless).  Fragments double-buffered: step t + 1's reads go out before step t's MFMAs, one
 // lgkmcnt(0) after them (as conv_rows_bf16).
+#ifndef EOSV_BNECK_LEAD
+#define EOSV_BNECK_LEAD 0  // r06 A/B: bitwise equal, R50 neutral (profiles/r06aa_fragment_lead.txt)
+#endif
 __device__ __forceinline__ void conv2_ring(const unsigned char* T1, const int (&rowb)[3], int r, int q,
                                            const bf16x8 (&wf)[18], f32x4 (&acc)[4], bool skip) {
   int e[3];
@@ -85,6 +88,32 @@ __device__ __forceinline__ void conv2_ring(const unsigned char* T1, const int (&
   for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (skip) return;
   bf16x8 bf[2][4];
+#if EOSV_BNECK_LEAD
+  // r06: fragment (t2 + 2, u) is read into the slot of (t2, u) right behind the MFMA that last reads
+  // it, so every read has 7 reads of lead and hipcc waits lgkmcnt(7) per MFMA instead of lgkmcnt(0)
+  // per k-step (as bblock2_bf16_kernel; same registers, same MFMAs per accumulator in the same order)
+  auto rd1 = [&](int t2, int u) __attribute__((always_inline)) {
+    const int tap = t2 >> 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+    return *(const bf16x8*)(T1 + rowb[dy] + ((t2 & 1) ? (e[dx] ^ 64) : e[dx]) + 2048 * u);
+  };
+#pragma unroll
+  for (int u = 0; u < 4; ++u) bf[0][u] = rd1(0, u);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) bf[1][u] = rd1(1, u);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t2 = 0; t2 < 18; ++t2) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t2], bf[t2 & 1][u], acc[u], 0, 0, 0);
+      if (t2 + 2 < 18) bf[t2 & 1][u] = rd1(t2 + 2, u);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (t2 + 2 < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return;
+#endif
   rd(0, bf[0]);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_sched_barrier(0);

@@ -10,6 +10,13 @@
 
 namespace eosv {
 
+// r06 A/B (release variants): the bf16 WS / tap-shift tiles issue a group's next A fragment read
+// ahead of all of the group's MFMAs (1, r06 default: R18 +0.4 %, R50 neutral, bitwise equal;
+// profiles/r06ab_rfirst.txt) or after its first (0, r04-r06)
+#ifndef EOSV_BF16_RFIRST
+#define EOSV_BF16_RFIRST 1
+#endif
+
 // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt split over bits 3:0 and 15:14, expcnt / lgkmcnt left
 // at their "no wait" maxima).  Through the builtin, not inline asm, so that hipcc's waitcnt pass
 // sees it and knows which loads it retired: after an asm wait hipcc still waited for them itself,

@@ -704,9 +704,14 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ws_kernel(ConvA
         }
         if (!EOSV_BF16_WS_BEARLY && g > 0 && g % TM == 0) rdB(g / TM);  // slice boundary: this slice's B (not overlapped)
         if (g + 1 < NG) afr[(g + 1) & 1] = rdA(g + 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (g + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+        if constexpr (EOSV_BF16_RFIRST) {  // r06 A/B: the next A fragment's read ahead of all TN MFMAs
+          if (g + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (g + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[g & 1], bfr[j], acc[i][j], 0, 0, 0);

@@ -541,9 +541,14 @@ __global__ __launch_bounds__(64 * (WM * WN + NP)) void conv_bf16_ts_ws_kernel(Co
       for (int i = 0; i < TM; ++i) {
 #endif
         if (i + 1 < TM) afr[(i + 1) & 1] = rdA(i + 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (i + 1 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+        if constexpr (EOSV_BF16_RFIRST) {  // r06 A/B: the next A fragment's read ahead of all TN MFMAs
+          if (i + 1 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (i + 1 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i & 1], bfr[j], acc[i][j], 0, 0, 0);

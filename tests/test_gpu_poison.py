@@ -77,3 +77,12 @@ def test_bblock_bitwise_equal_unfused(name, tmp_path):
     kernels at 256): every stage map bitwise equal, one image per workgroup (37 frames) and several
     (601 / 300 frames: the stream crosses images through the zero step)."""
     _switch_stage_maps_equal("EOSV_BBLOCK", name, tmp_path, "bblock", "two-launch stage-1")
+
+
+@pytest.mark.parametrize("name", ["resnet18:224:601", "resnet18:256:300"])
+def test_bblock2_bitwise_equal_bblock(name, tmp_path):
+    """r06: the split-conv basic block (bblock2_bf16_kernel: one conv per wave for 32 couts, the two
+    convs of different steps in one phase, the rolling fragment lead) against the one-wave-both-convs
+    kernel it replaces (EOSV_BBLOCK2=0): every stage map bitwise equal at 56x56 and 64x64, with the
+    stream crossing images (601 / 300 frames on 256 CUs)."""
+    _switch_stage_maps_equal("EOSV_BBLOCK2", name, tmp_path, "bblock2", "bblock")
