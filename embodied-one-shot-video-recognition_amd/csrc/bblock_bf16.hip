@@ -311,6 +311,9 @@ struct Bb2Geo {
 
 // timing-only ablations of release variants (results wrong): 1 no MFMAs, 2 no fragment reads after
 // the first, 4 no phase barriers
+#ifndef EOSV_BB2_PRIO
+#define EOSV_BB2_PRIO 0
+#endif
 #ifndef EOSV_BB2_LEAD
 #define EOSV_BB2_LEAD 1
 #endif
@@ -543,6 +546,11 @@ __global__ __launch_bounds__(64 * BB_NW) void bblock2_bf16_kernel(BneckArgs a) {
   // before the ring writes is the counted vmcnt(8) -- stores inside the conv2 branch gave it a path
   // without them, and a vmcnt(0) at the top of every phase (as bblock_bf16_kernel's note says)
   const __amdgpu_buffer_rsrc_t nowhere = bb_rsrc(a.y, 0);
+  if constexpr (EOSV_BB2_PRIO == 1) {  // r06 A/B: the conv2 waves first at the SIMD's issue
+    if (grp) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (EOSV_BB2_PRIO == 2) {  // ... or the conv1 waves
+    if (!grp) __builtin_amdgcn_s_setprio(1);
+  }
   for (int g = 0; g <= total; ++g) {
     vm_wait<8>();  // S has landed: younger are only the previous phase's stores
     put_x(g + 3, S);
