@@ -15,7 +15,7 @@ dispatches inside it, and their number must equal the line's roofline.conv_launc
 its traffic_algorithmic covers) -- nothing is back-filled from warmup or setup dispatches.  The
 family is every kernel the library's conv profile records cover (the stems, the implicit GEMMs,
 the row / strip kernels and the fused pairs: names starting conv_, stem_pool_, pair1x1 (both
-pair1x1_bf16 and the r04 pair1x1r_bf16), pairw_, bneck_ or bblock_ (the r06 whole-block stage-1
+pair1x1_bf16 and the r04 pair1x1r_bf16), pairw_, bneck_, bblock_ or bblock2_ (the r06 whole-block stage-1
 kernels));
 the other kernels of the window (clip
 embedding, matching) are listed under "other_in_window".
@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "embodied-one-shot-video-recognition_amd"))
 from eosv._lib import library_digest, library_kind, source_digest  # noqa: E402
 
-FAMILY = ("conv_", "stem_pool_", "pair1x1", "pairw_", "bneck_", "bblock_")
+FAMILY = ("conv_", "stem_pool_", "pair1x1", "pairw_", "bneck_", "bblock_", "bblock2_")
 BEGIN, END = "profile_window_begin_kernel", "profile_window_end_kernel"
 
 
